@@ -1,0 +1,221 @@
+"""3ddctvideoencoding_amd -- MI355X-native 3D-DCT hot path of julianopiccoli/3dDCTVideoEncoding.
+
+The product is the C-ABI library ``lib/libdct3d.so`` (HIP kernels for gfx950 + runtime, declared in
+``include/dct3d.h``) and the reference-compatible C codec host ``lib/libdct3dcodec.so`` /
+``lib/dct3d_codec``.  This module is a thin ctypes binding with the same entry-point names; it has
+NO fallback: if the library is missing or no HIP device is present the calls raise.
+
+Since the package name starts with a digit, import it with
+``importlib.import_module("3ddctvideoencoding_amd")``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from . import synthetic  # noqa: F401  (integer-only generator shared with the device kernel)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libdct3d.so")
+CODEC_LIB_PATH = os.path.join(LIB_DIR, "libdct3dcodec.so")
+CLI_PATH = os.path.join(LIB_DIR, "dct3d_codec")
+REPO_DIR = os.path.dirname(PKG_DIR)
+INCLUDE_DIR = os.path.join(REPO_DIR, "include")
+
+DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL = 0, 1, 2, 3, 4
+
+# Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = (
+    "dct3d_abi_version", "dct3d_strerror", "dct3d_ctx_create", "dct3d_ctx_destroy",
+    "dct3d_ctx_set_stream", "dct3d_ctx_set_profiling", "dct3d_synchronize", "dct3d_get_stats",
+    "dct3d_reset_timers",
+    "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
+    "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
+    "dct3d_fill_synthetic_dev",
+)
+
+
+class Dct3dError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {strerror(code)} ({code})")
+        self.code = code
+
+
+class Stats(C.Structure):
+    _fields_ = [("n_units", C.c_uint64), ("n_flagged", C.c_uint64), ("n_overflow_cubes", C.c_uint64),
+                ("n_timed", C.c_uint64), ("kernel_ms_total", C.c_double), ("fixup_ms_total", C.c_double)]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libdct3d.so (raises if it has not been built: run __graft_entry__.build() / make)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        vp, i32, sz, u64, i64 = C.c_void_p, C.c_int, C.c_size_t, C.c_uint64, C.c_int64
+        L.dct3d_abi_version.restype = i32
+        L.dct3d_strerror.restype = C.c_char_p
+        L.dct3d_strerror.argtypes = [i32]
+        L.dct3d_ctx_create.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
+        L.dct3d_ctx_destroy.argtypes = [vp]
+        L.dct3d_ctx_destroy.restype = None
+        L.dct3d_ctx_set_stream.argtypes = [vp, vp]
+        L.dct3d_ctx_set_profiling.argtypes = [vp, i32]
+        L.dct3d_synchronize.argtypes = [vp]
+        L.dct3d_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.dct3d_reset_timers.argtypes = [vp]
+        for name in ("dct3d_encode_stacks", "dct3d_encode_stacks_dev"):
+            getattr(L, name).argtypes = [vp, vp, i32, i32, i32, vp, vp]
+        for name in ("dct3d_decode_stacks", "dct3d_decode_stacks_dev"):
+            getattr(L, name).argtypes = [vp, vp, i32, i32, i32, vp]
+        for name in ("dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev"):
+            getattr(L, name).argtypes = [vp, vp, sz, vp]
+        L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
+        _lib = L
+    return _lib
+
+
+def strerror(code: int) -> str:
+    try:
+        return lib().dct3d_strerror(code).decode()
+    except Exception:
+        return "error"
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != DCT3D_OK:
+        raise Dct3dError(rc, what)
+
+
+def _ptr(a: np.ndarray) -> int:
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return a.ctypes.data
+
+
+def _tptr(t) -> int:
+    """device pointer of a torch tensor (or an int address)."""
+    if isinstance(t, int):
+        return t
+    if not t.is_contiguous():
+        raise ValueError("tensor must be contiguous")
+    return t.data_ptr()
+
+
+class Context:
+    """dct3d_ctx: one per device (the MI355X equivalent of the reference's per-call OpenCL setup,
+    encoder.c:169-219).  Block dims are codec.h's DCT_BLOCK_WIDTH/HEIGHT/DEPTH (8x8x8 or 8x8x4)."""
+
+    def __init__(self, device: int = 0, block_w: int = 8, block_h: int = 8, block_d: int = 8):
+        h = C.c_void_p()
+        _check(lib().dct3d_ctx_create(device, block_w, block_h, block_d, C.byref(h)), "dct3d_ctx_create")
+        self._h = h
+        self.device, self.bw, self.bh, self.bd = device, block_w, block_h, block_d
+        self.cube_size = block_w * block_h * block_d
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().dct3d_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- configuration ----
+    def set_stream(self, hip_stream: Optional[int]) -> None:
+        _check(lib().dct3d_ctx_set_stream(self._h, hip_stream or None), "dct3d_ctx_set_stream")
+
+    def set_profiling(self, on: bool) -> None:
+        _check(lib().dct3d_ctx_set_profiling(self._h, 1 if on else 0), "dct3d_ctx_set_profiling")
+
+    def synchronize(self) -> None:
+        _check(lib().dct3d_synchronize(self._h), "dct3d_synchronize")
+
+    def stats(self) -> dict:
+        st = Stats()
+        _check(lib().dct3d_get_stats(self._h, C.byref(st)), "dct3d_get_stats")
+        return st.as_dict()
+
+    def reset_timers(self) -> None:
+        _check(lib().dct3d_reset_timers(self._h), "dct3d_reset_timers")
+
+    def n_cubes(self, width: int, height: int, n_stacks: int) -> int:
+        return (width // self.bw) * (height // self.bh) * n_stacks
+
+    # ---- host-pointer (synchronous) entry points ----
+    def encode_stacks(self, frames: np.ndarray, want_dct: bool = False):
+        """u8 frames [n_stacks*bd, H, W] -> quantised int32 cubes [n_cubes, bd, bh, bw]
+        (+ fp64 DCT coefficients in the same layout when want_dct)."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        F, H, W = frames.shape
+        if F % self.bd:
+            raise ValueError("frame count must be a multiple of the block depth")
+        n = self.n_cubes(W, H, F // self.bd)
+        q = np.empty((n, self.bd, self.bh, self.bw), np.int32)
+        d = np.empty((n, self.bd, self.bh, self.bw), np.float64) if want_dct else None
+        _check(lib().dct3d_encode_stacks(self._h, _ptr(frames), W, H, F // self.bd, _ptr(q),
+                                         _ptr(d) if want_dct else None), "dct3d_encode_stacks")
+        return (q, d) if want_dct else q
+
+    def decode_stacks(self, q: np.ndarray, width: int, height: int, n_stacks: int) -> np.ndarray:
+        q = np.ascontiguousarray(q, np.int32)
+        out = np.empty((n_stacks * self.bd, height, width), np.uint8)
+        _check(lib().dct3d_decode_stacks(self._h, _ptr(q), width, height, n_stacks, _ptr(out)),
+               "dct3d_decode_stacks")
+        return out
+
+    def forward_f32(self, cubes: np.ndarray) -> np.ndarray:
+        cubes = np.ascontiguousarray(cubes, np.float32)
+        n = cubes.size // self.cube_size
+        out = np.empty_like(cubes)
+        _check(lib().dct3d_forward_f32(self._h, _ptr(cubes), n, _ptr(out)), "dct3d_forward_f32")
+        return out
+
+    def inverse_f32(self, coeffs: np.ndarray) -> np.ndarray:
+        coeffs = np.ascontiguousarray(coeffs, np.float32)
+        n = coeffs.size // self.cube_size
+        out = np.empty_like(coeffs)
+        _check(lib().dct3d_inverse_f32(self._h, _ptr(coeffs), n, _ptr(out)), "dct3d_inverse_f32")
+        return out
+
+    # ---- device-pointer (asynchronous, ctx stream) entry points ----
+    def encode_stacks_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q, d_dct=None) -> None:
+        _check(lib().dct3d_encode_stacks_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q),
+                                             _tptr(d_dct) if d_dct is not None else None),
+               "dct3d_encode_stacks_dev")
+
+    def decode_stacks_dev(self, d_q, width: int, height: int, n_stacks: int, d_frames) -> None:
+        _check(lib().dct3d_decode_stacks_dev(self._h, _tptr(d_q), width, height, n_stacks, _tptr(d_frames)),
+               "dct3d_decode_stacks_dev")
+
+    def forward_f32_dev(self, d_in, n_cubes: int, d_out) -> None:
+        _check(lib().dct3d_forward_f32_dev(self._h, _tptr(d_in), n_cubes, _tptr(d_out)), "dct3d_forward_f32_dev")
+
+    def inverse_f32_dev(self, d_in, n_cubes: int, d_out) -> None:
+        _check(lib().dct3d_inverse_f32_dev(self._h, _tptr(d_in), n_cubes, _tptr(d_out)), "dct3d_inverse_f32_dev")
+
+    def fill_synthetic_dev(self, d_frames, width: int, height: int, n_frames: int,
+                           seed: int = synthetic.DEFAULT_SEED, frame0: int = 0, kind: str = "ramp") -> None:
+        k = {"ramp": 0, "uniform": 1}[kind]
+        _check(lib().dct3d_fill_synthetic_dev(self._h, _tptr(d_frames), width, height, n_frames, seed, frame0, k),
+               "dct3d_fill_synthetic_dev")

@@ -1,0 +1,85 @@
+// dct3d_kernels.h -- kernel parameter blocks and launchers (shared by dct3d_kernels.hip and the
+// C-ABI runtime dct3d_runtime.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dct3d {
+
+constexpr int kMaxGroupsDev = 64;  // == kMaxGroups in dct3d_plan.h; one LDS slot per lane
+
+struct EncodeParams {
+    const uint8_t* raster;
+    int32_t* out;
+    uint32_t n_cubes;          // cubes in this launch (whole stacks)
+    uint32_t cubes_per_stack;
+    uint32_t nbx;              // cubes per block-row
+    uint32_t width;
+    uint64_t plane;            // width * height
+    uint64_t stack_stride;     // D * plane
+    double coef_dc;            // Java DC group coefficient
+    const float* tab_rstep;    // [32] fp32(1/step_s)
+    const float* tab_G;        // [32]
+    const float* tab_E;        // [32]
+    unsigned long long* flag_list;
+    unsigned int* counters;    // [0] flagged coefficients, [1] overflow cubes
+    uint32_t flag_cap;
+    uint32_t* cube_list;       // capacity n_cubes
+};
+
+struct FixupParams {
+    const uint8_t* raster;
+    int32_t* out;
+    uint32_t cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+    const unsigned long long* flag_list;
+    const unsigned int* counters;
+    uint32_t flag_cap;
+    const uint32_t* cube_list;
+    const int32_t* ngroups;    // [cs]
+    const double* coef;        // [cs * kMaxGroupsDev]
+    const uint8_t* group_of;   // [cs * cs]
+};
+
+struct DecodeParams {
+    const int32_t* in;
+    uint8_t* out;
+    uint32_t n_cubes, cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+    double dec_G, dec_E;
+    unsigned long long* flag_list;
+    unsigned int* counters;
+    uint32_t flag_cap;
+    uint32_t* cube_list;
+};
+
+struct DecodeFixupParams {
+    const int32_t* in;
+    uint8_t* out;
+    uint32_t cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+    const unsigned long long* flag_list;
+    const unsigned int* counters;
+    uint32_t flag_cap;
+    const uint32_t* cube_list;
+    const double* inv_coef;    // [cs * cs]
+};
+
+struct Fwd64Params {
+    const uint8_t* raster;
+    double* out;
+    uint32_t n_cubes, cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+};
+
+int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st);
+int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
+int launch_encode(int D, const EncodeParams& P, hipStream_t st);
+int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
+int launch_decode(int D, const DecodeParams& P, hipStream_t st);
+int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
+int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,
+                 hipStream_t st);
+
+}  // namespace dct3d

@@ -1,0 +1,673 @@
+// dct3d_kernels.hip -- CDNA4 (gfx950) kernels of the 3D-DCT hot path.
+//
+// Work decomposition (all transform kernels): one wave64 owns 8 cubes, 8 lanes per cube.
+//   "row layout"  lane (c, y)        holds a[z][x]   (D x 8 values): the cube's row y of every frame
+//   "face layout" lane (c, kz[,h])   holds b[y][x]   (8 x 8 or 8 x 4 values): one z-face (or half)
+// Two of the three separable 8-point passes run in registers in one layout, the third in the other;
+// the single layout change is a wave-private LDS transpose (no workgroup barrier: one wave writes
+// and reads its own region, LDS ops of a wave execute in order).  Cube-major int32 / fp64 traffic is
+// staged through the same LDS region so every global access of the wave is a contiguous 1 KiB
+// (16 B per lane) burst; the u8 raster side is 8 B per lane, 8 rows x 64 B per instruction.
+//
+// Encode (raster u8 -> quantised int32 cube-major), fp32, certified:
+//   load rows (row layout) -> cube sum S, mean m, A = max|x - m| (xor-shuffles over the 8 lanes)
+//   -> pass X (exact integer front, centring folded into X0) -> pass Z -> LDS transpose
+//   -> pass Y (face layout) -> quantise: q = v * fp32(1/step), n = rint(q), certify |q - n| < thr_s
+//   where thr_s = 0.5 - (A*G_s + E_s) (dct3d_plan.cpp) -> LDS staging -> 1 KiB coalesced stores.
+//   DC = JavaRound(fp64(S) * coef_dc) exactly (the Java fold of the single DC group).
+//   Uncertified coefficients are appended to a flag list; encode_fixup_kernel replays the Java fold.
+// Decode (quantised int32 cube-major -> raster u8), fp64, certified:
+//   staged 1 KiB loads -> face layout -> dequantise -> inverse pass Y -> LDS transpose (4 quarter
+//   rounds, 16 B per lane-slot) -> inverse pass X -> inverse pass Z -> certify (no integer within
+//   the bound of the pixel value in [1,255]) -> clamp, truncate (Decoder.java:112) -> 8 B row stores.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dct_butterfly.h"
+#include "dct3d_kernels.h"
+
+namespace dct3d {
+
+constexpr int kWave = 64;
+constexpr int kCubesPerWave = 8;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+constexpr int kSlot = 144;                 // transpose slot: 8 rows x 16 B + 16 B pad (bank spread)
+constexpr int kWaveLds = kSlot * 64;       // 9216 B per wave
+constexpr int kFace = 272;                 // staging face: 256 B + 16 B pad
+static_assert(4 * 8 * kFace <= kWaveLds, "staging round must fit the wave region");
+
+// Wave-level ordering of LDS traffic between lanes of ONE wave: a compiler fence (LDS instructions
+// of a wave are executed in order, so no s_waitcnt is needed for visibility within the wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Java Math.round(double) (round half up, exact)
+__device__ __forceinline__ int java_round_dev(double a) {
+    double f = floor(a);
+    return (int)f + ((a - f) >= 0.5 ? 1 : 0);
+}
+
+// Register "pins": an empty volatile asm that redefines the values passed to it.  Volatile asms keep
+// program order, so pinning a butterfly's inputs before it and its outputs after it serialises the
+// butterflies of a pass (the compiler otherwise interleaves all of them and multiplies the live
+// temporaries, which costs occupancy).
+template <class T, int N>
+__device__ __forceinline__ void pin(T (&x)[N]) {
+    if constexpr (sizeof(T) == 4) {
+        if constexpr (N == 8)
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]));
+        else
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+    } else {
+        if constexpr (N == 8)
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]));
+        else
+            asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+    }
+}
+
+__device__ __forceinline__ float byte_of(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
+
+// =============================================================================================
+// Fused encode
+// =============================================================================================
+// Loads row y = j of frames 0..D-1 of cube g (row layout).
+template <int D>
+__device__ __forceinline__ void load_rows(const EncodeParams& P, uint32_t g, bool valid, int j, uint2 (&raw)[D]) {
+    if (valid) {
+        const uint32_t s = g / P.cubes_per_stack;
+        const uint32_t r = g - s * P.cubes_per_stack;
+        const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
+        const uint8_t* src = P.raster + (size_t)s * P.stack_stride + (size_t)(by * 8 + j) * P.width + bx * 8;
+#pragma unroll
+        for (int z = 0; z < D; z++) raw[z] = *(const uint2*)(src + (size_t)z * P.plane);
+    } else {
+#pragma unroll
+        for (int z = 0; z < D; z++) raw[z] = make_uint2(0u, 0u);
+    }
+}
+
+// Cube statistics over the 8 lanes of a cube: S = sum, m = integer mean, A = max |x - m|.
+template <int D>
+__device__ __forceinline__ void cube_stats(const uint2 (&raw)[D], uint32_t& S, int& m, float& A) {
+    constexpr int CS = 64 * D;
+    S = 0;
+    uint32_t mx = 0, mn = 255;
+#pragma unroll
+    for (int z = 0; z < D; z++) {
+        S = __builtin_amdgcn_udot4(raw[z].x, 0x01010101u, S, false);
+        S = __builtin_amdgcn_udot4(raw[z].y, 0x01010101u, S, false);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t v0 = (raw[z].x >> (8 * b)) & 0xFFu, v1 = (raw[z].y >> (8 * b)) & 0xFFu;
+            mx = max(mx, max(v0, v1));
+            mn = min(mn, min(v0, v1));
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+        S += __shfl_xor(S, o, 64);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    }
+    m = (int)((S + CS / 2) / CS);
+    A = (float)max((int)mx - m, m - (int)mn);
+}
+
+// Full forward transform of the wave's 8 cubes: row layout -> face layout coefficients b[ky][kx'].
+// Uses the wave's LDS region (no cross-wave sharing).
+template <int D, int NB>
+__device__ __forceinline__ void forward_cube(const uint2 (&raw)[D], int m, int c, int j, char* wl, float (&b)[8][NB]) {
+    float a[D][8];
+#pragma unroll
+    for (int z = 0; z < D; z++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            a[z][e] = byte_of(raw[z].x, e);
+            a[z][e + 4] = byte_of(raw[z].y, e);
+        }
+    const float dcsub = 8.0f * (float)m;
+    // pass X (integer front exact, cube-mean centring folded into X0), pass Z
+#pragma unroll
+    for (int z = 0; z < D; z++) {
+        pin(a[z]);
+        fdct8<true, true>(a[z], dcsub);
+        pin(a[z]);
+    }
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        float col[D];
+#pragma unroll
+        for (int z = 0; z < D; z++) col[z] = a[z][x];
+        pin(col);
+        fdctN<D, false, false>(col, 0.f);
+        pin(col);
+#pragma unroll
+        for (int z = 0; z < D; z++) a[z][x] = col[z];
+    }
+    // LDS transpose: row layout (c, y)[kz][x] -> face layout (c, j)[y][kx']
+    if constexpr (D == 8) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int kz = 0; kz < 8; kz++)
+                *(float4*)(wl + (c * 8 + kz) * kSlot + j * 16) =
+                    make_float4(a[kz][4 * h], a[kz][4 * h + 1], a[kz][4 * h + 2], a[kz][4 * h + 3]);
+            wave_lds_sync();
+#pragma unroll
+            for (int y = 0; y < 8; y++) {
+                float4 t = *(const float4*)(wl + (c * 8 + j) * kSlot + y * 16);
+                b[y][4 * h] = t.x; b[y][4 * h + 1] = t.y; b[y][4 * h + 2] = t.z; b[y][4 * h + 3] = t.w;
+            }
+            wave_lds_sync();
+        }
+    } else {
+#pragma unroll
+        for (int kz = 0; kz < 4; kz++)
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                *(float4*)(wl + ((c * 4 + kz) * 2 + h) * kSlot + j * 16) =
+                    make_float4(a[kz][4 * h], a[kz][4 * h + 1], a[kz][4 * h + 2], a[kz][4 * h + 3]);
+        wave_lds_sync();
+#pragma unroll
+        for (int y = 0; y < 8; y++) {
+            float4 t = *(const float4*)(wl + (c * 8 + j) * kSlot + y * 16);
+            b[y][0] = t.x; b[y][1] = t.y; b[y][2] = t.z; b[y][3] = t.w;
+        }
+        wave_lds_sync();
+    }
+    // pass Y
+#pragma unroll
+    for (int x = 0; x < NB; x++) {
+        float col[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = b[y][x];
+        pin(col);
+        fdct8<false, false>(col, 0.f);
+        pin(col);
+#pragma unroll
+        for (int y = 0; y < 8; y++) b[y][x] = col[y];
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void encode_kernel(EncodeParams P) {
+    constexpr int CS = 64 * D;
+    constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
+    constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = lane >> 3, j = lane & 7;
+    char* wl = lds + wave * kWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+
+    uint2 raw[D];
+    load_rows<D>(P, g, valid, j, raw);
+    uint32_t S;
+    int m;
+    float A;
+    cube_stats<D>(raw, S, m, A);
+    asm volatile("" : "+v"(S), "+v"(m), "+v"(A));  // compute the stats now: raw dies after conversion
+
+    float b[8][NB];
+    forward_cube<D, NB>(raw, m, c, j, wl, b);
+
+    // ---- quantise + certify (in place: b becomes the integer coefficients) ----
+    const int kz = (D == 8) ? j : (j >> 1);
+    const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
+    const int so = kz + kx0;
+    float rr[NI], thr[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        rr[i] = P.tab_rstep[so + i];
+        thr[i] = __builtin_fmaf(-A, P.tab_G[so + i], 0.5f - P.tab_E[so + i]);
+    }
+    int32_t qv[8][NB];
+    int flag = 0;
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++) {
+        pin(b[ky]);
+        bool f = false;
+#pragma unroll
+        for (int x = 0; x < NB; x++) {
+            const float q = b[ky][x] * rr[ky + x];
+            const float n = __builtin_rintf(q);
+            f |= __builtin_fabsf(q - n) >= thr[ky + x];
+            qv[ky][x] = (int32_t)n;
+        }
+        flag |= (int)f;
+        pin(qv[ky]);
+        asm volatile("" : "+v"(flag));  // the row's checks complete here (q, n die)
+    }
+    if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+
+    // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
+    constexpr int ROUNDS = (D == 8) ? 2 : 1;
+    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
+#pragma unroll
+    for (int rd = 0; rd < ROUNDS; rd++) {
+        if ((c / CUBES_PER_ROUND) == rd) {
+            const int cc = c % CUBES_PER_ROUND;
+            if constexpr (D == 8) {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+                        *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
+                            make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
+            } else {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+                    *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
+                        make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
+            }
+        }
+        wave_lds_sync();
+        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
+        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
+            const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
+            const int face = (q >> 4) % D;
+            const int w = q & 15;
+            if (rcube0 + cc < P.n_cubes) {
+                const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
+                *(int4*)(outb + (size_t)q * 16) = v;
+            }
+        }
+        wave_lds_sync();
+    }
+
+    // ---- rare path: identify uncertified coefficients (recomputed from the raw rows) ----
+    if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
+        uint2 raw2[D];
+        load_rows<D>(P, g, valid, j, raw2);  // reload (rare path) instead of keeping 2*D VGPRs live
+        float b2[8][NB];
+        forward_cube<D, NB>(raw2, m, c, j, wl, b2);
+        bool overflow = false;
+        if (flag && valid) {
+#pragma unroll
+            for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                for (int x = 0; x < NB; x++) {
+                    const float rr2 = P.tab_rstep[so + ky + x];
+                    const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
+                    const float q = b2[ky][x] * rr2;
+                    const float n = __builtin_rintf(q);
+                    if (__builtin_fabsf(q - n) >= th2) {
+                        const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
+                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
+                        else overflow = true;
+                    }
+                }
+        }
+        // at most one cube-list entry per cube: the lowest overflowing lane of the cube appends
+        const unsigned long long ov = __ballot(overflow);
+        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
+        if (overflow && (__builtin_ctz(mine) == j)) {
+            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
+        }
+    }
+}
+
+// =============================================================================================
+// Exact Java fold for flagged (cube, k): out = JavaRound(fold_g(S_g * coef_g) / step)
+// =============================================================================================
+template <int D>
+__global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
+    constexpr int CS = 64 * D;
+    __shared__ int Ssum[4][kMaxGroupsDev];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nf = min(P.counters[0], P.flag_cap);
+    const uint32_t ncube = P.counters[1];
+    const unsigned long long total = (unsigned long long)nf + (unsigned long long)ncube * CS;
+    for (unsigned long long e = (unsigned long long)blockIdx.x * 4 + wave; e < total;
+         e += (unsigned long long)gridDim.x * 4) {
+        uint32_t g, k;
+        if (e < nf) {
+            const unsigned long long v = P.flag_list[e];
+            g = (uint32_t)(v / CS);
+            k = (uint32_t)(v % CS);
+        } else {
+            const unsigned long long e2 = e - nf;
+            g = P.cube_list[e2 / CS];
+            k = (uint32_t)(e2 % CS);
+        }
+        Ssum[wave][lane] = 0;
+        wave_lds_sync();
+        if (lane * 8 < CS) {
+            const int z = lane >> 3, y = lane & 7;
+            const uint32_t s = g / P.cubes_per_stack;
+            const uint32_t r = g - s * P.cubes_per_stack;
+            const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
+            const uint8_t* src = P.raster + (size_t)s * P.stack_stride + (size_t)z * P.plane +
+                                 (size_t)(by * 8 + y) * P.width + bx * 8;
+            const uint2 px = *(const uint2*)src;
+            const uint2 gr = *(const uint2*)(P.group_of + (size_t)k * CS + lane * 8);
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+                const uint32_t g0 = (gr.x >> (8 * bb)) & 0xFF, g1 = (gr.y >> (8 * bb)) & 0xFF;
+                if (g0 < kMaxGroupsDev) atomicAdd(&Ssum[wave][g0], (int)((px.x >> (8 * bb)) & 0xFF));
+                if (g1 < kMaxGroupsDev) atomicAdd(&Ssum[wave][g1], (int)((px.y >> (8 * bb)) & 0xFF));
+            }
+        }
+        wave_lds_sync();
+        if (lane == 0) {
+            const int ng = P.ngroups[k];
+            double acc = 0.0;
+            for (int gi = 0; gi < ng; gi++) {
+                const double prod = __dmul_rn((double)Ssum[wave][gi], P.coef[(size_t)k * kMaxGroupsDev + gi]);
+                acc = __dadd_rn(acc, prod);  // DCT.java:50: output += sum * coefficient
+            }
+            const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+            const int st = max(1, 5 * (kx + ky + kz));
+            P.out[(size_t)g * CS + k] = java_round_dev(__ddiv_rn(acc, (double)st));
+        }
+        wave_lds_sync();
+    }
+}
+
+// =============================================================================================
+// Fused decode (fp64, certified)
+// =============================================================================================
+template <int D>
+__global__ __launch_bounds__(kBlock) void decode_kernel(DecodeParams P) {
+    constexpr int CS = 64 * D;
+    constexpr int NB = (D == 8) ? 8 : 4;
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = lane >> 3, j = lane & 7;
+    char* wl = lds + wave * kWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+    const int kz = (D == 8) ? j : (j >> 1);
+    const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
+
+    // ---- staged loads: 8 KiB rounds, 1 KiB per instruction, into the face-padded layout ----
+    constexpr int ROUNDS = (D == 8) ? 2 : 1;
+    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
+    double b[8][NB];
+    double amax = 0.0;
+#pragma unroll
+    for (int rd = 0; rd < ROUNDS; rd++) {
+        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
+        const char* inb = (const char*)(P.in + (size_t)rcube0 * CS);
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int q = t * 64 + lane;
+            const int cc = q / (CS / 4);
+            const int face = (q >> 4) % D;
+            const int w = q & 15;
+            int4 v = make_int4(0, 0, 0, 0);
+            if (rcube0 + cc < P.n_cubes) v = *(const int4*)(inb + (size_t)q * 16);
+            *(int4*)(wl + (cc * D + face) * kFace + w * 16) = v;
+        }
+        wave_lds_sync();
+        if ((c / CUBES_PER_ROUND) == rd) {
+            const int cc = c % CUBES_PER_ROUND;
+#pragma unroll
+            for (int ky = 0; ky < 8; ky++) {
+                if constexpr (D == 8) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int4 v = *(const int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16);
+                        const int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int e = 0; e < 4; e++) {
+                            const int kx = 4 * h + e;
+                            const double cf = (double)vv[e] * (double)max(1, 5 * (kx + ky + kz));
+                            b[ky][4 * h + e] = cf;
+                            amax = fmax(amax, fabs(cf));
+                        }
+                    }
+                } else {
+                    const int4 v = *(const int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16);
+                    const int vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int kx = kx0 + e;
+                        const double cf = (double)vv[e] * (double)max(1, 5 * (kx + ky + kz));
+                        b[ky][e] = cf;
+                        amax = fmax(amax, fabs(cf));
+                    }
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o, 64));
+
+    // ---- inverse pass Y (face layout) ----
+#pragma unroll
+    for (int x = 0; x < NB; x++) {
+        double col[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = b[y][x];
+        idct8(col);
+#pragma unroll
+        for (int y = 0; y < 8; y++) b[y][x] = col[y];
+    }
+
+    // ---- LDS transpose in 4 quarter rounds (kx pairs): face layout -> row layout (c, y)[kz][kx] ----
+    double a[D][8];
+#pragma unroll
+    for (int qr = 0; qr < 4; qr++) {
+        const bool writer = (D == 8) || ((j & 1) == (qr >> 1));
+        if (writer) {
+            const int xl = (D == 8) ? 2 * qr : 2 * (qr & 1);  // local kx index inside b
+#pragma unroll
+            for (int y = 0; y < 8; y++)
+                *(double2*)(wl + (c * 8 + y) * kSlot + kz * 16) = make_double2(b[y][xl], b[y][xl + 1]);
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int z = 0; z < D; z++) {
+            const double2 t = *(const double2*)(wl + (c * 8 + j) * kSlot + z * 16);
+            a[z][2 * qr] = t.x;
+            a[z][2 * qr + 1] = t.y;
+        }
+        wave_lds_sync();
+    }
+
+    // ---- inverse pass X, inverse pass Z (row layout, y = j) ----
+#pragma unroll
+    for (int z = 0; z < D; z++) idct8(a[z]);
+#pragma unroll
+    for (int x = 0; x < 8; x++) {
+        double col[D];
+#pragma unroll
+        for (int z = 0; z < D; z++) col[z] = a[z][x];
+        idctN<D>(col);
+#pragma unroll
+        for (int z = 0; z < D; z++) a[z][x] = col[z];
+    }
+
+    // ---- certify, clamp + truncate (InverseDCT.java:74-80, Decoder.java:112), store rows ----
+    const double margin = amax * P.dec_G + P.dec_E;
+    bool flag = false;
+    uint2 outw[D];
+#pragma unroll
+    for (int z = 0; z < D; z++) {
+        uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+        for (int x = 0; x < 8; x++) {
+            const double v = a[z][x];
+            const double r = rint(v);
+            flag |= (r >= 1.0) & (r <= 255.0) & (fabs(v - r) <= margin);
+            const uint32_t px = v <= 0.0 ? 0u : (v >= 255.0 ? 255u : (uint32_t)v);
+            if (x < 4) w0 |= px << (8 * x);
+            else w1 |= px << (8 * (x - 4));
+        }
+        outw[z] = make_uint2(w0, w1);
+    }
+    if (valid) {
+        const uint32_t s = g / P.cubes_per_stack;
+        const uint32_t r = g - s * P.cubes_per_stack;
+        const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
+        uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + j) * P.width + bx * 8;
+#pragma unroll
+        for (int z = 0; z < D; z++) *(uint2*)(dst + (size_t)z * P.plane) = outw[z];
+    }
+    if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
+        bool overflow = false;
+        if (flag && valid) {
+#pragma unroll
+            for (int z = 0; z < D; z++)
+#pragma unroll
+                for (int x = 0; x < 8; x++) {
+                    const double v = a[z][x];
+                    const double r = rint(v);
+                    if ((r >= 1.0) & (r <= 255.0) & (fabs(v - r) <= margin)) {
+                        const uint32_t n = (uint32_t)((z * 8 + j) * 8 + x);
+                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + n;
+                        else overflow = true;
+                    }
+                }
+        }
+        const unsigned long long ov = __ballot(overflow);
+        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
+        if (overflow && (__builtin_ctz(mine) == j)) {
+            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+            P.cube_list[idx] = g;
+        }
+    }
+}
+
+// Exact Java InverseDCT fold for flagged (cube, n): one lane per entry, k ascending, zeros skipped.
+template <int D>
+__global__ __launch_bounds__(256) void decode_fixup_kernel(DecodeFixupParams P) {
+    constexpr int CS = 64 * D;
+    const uint32_t nf = min(P.counters[0], P.flag_cap);
+    const uint32_t ncube = P.counters[1];
+    const unsigned long long total = (unsigned long long)nf + (unsigned long long)ncube * CS;
+    for (unsigned long long e = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (unsigned long long)gridDim.x * blockDim.x) {
+        uint32_t g, n;
+        if (e < nf) {
+            const unsigned long long v = P.flag_list[e];
+            g = (uint32_t)(v / CS);
+            n = (uint32_t)(v % CS);
+        } else {
+            const unsigned long long e2 = e - nf;
+            g = P.cube_list[e2 / CS];
+            n = (uint32_t)(e2 % CS);
+        }
+        const int32_t* q = P.in + (size_t)g * CS;
+        const double* row = P.inv_coef + (size_t)n * CS;
+        double acc = 0.0;
+        for (int k = 0; k < CS; k++) {
+            const int32_t qk = q[k];
+            if (qk != 0) {
+                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+                const double cf = (double)qk * (double)max(1, 5 * (kx + ky + kz));
+                acc = __dadd_rn(acc, __dmul_rn(cf, row[k]));  // InverseDCT.java:64
+            }
+        }
+        const double mn = acc < 255.0 ? acc : 255.0;
+        const double v = mn > 0.0 ? mn : 0.0;
+        const uint32_t s = g / P.cubes_per_stack;
+        const uint32_t r = g - s * P.cubes_per_stack;
+        const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
+        const int z = n / 64, y = (n / 8) & 7, x = n & 7;
+        P.out[(size_t)s * P.stack_stride + (size_t)z * P.plane + (size_t)(by * 8 + y) * P.width + bx * 8 + x] =
+            (uint8_t)(int)v;
+    }
+}
+
+// =============================================================================================
+// Synthetic frames (integer-only, reproducible on host)
+// =============================================================================================
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, int width, int height, long long n_pix, uint64_t seed,
+                                                     long long frame0, int kind) {
+    const long long plane = (long long)width * height;
+    for (long long base = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 16; base < n_pix;
+         base += (long long)gridDim.x * blockDim.x * 16) {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 16 && base + i < n_pix; i++) {
+            const long long p = base + i;
+            const long long f = p / plane + frame0;
+            const long long rem = p % plane;
+            const int y = (int)(rem / width), x = (int)(rem % width);
+            const uint64_t idx = (uint64_t)(frame0 * plane + p);
+            const uint64_t h = splitmix64(seed ^ idx);
+            int v;
+            if (kind == 1) v = (int)(h & 255u);
+            else {
+                v = 128 + (int)((3ll * x + 5ll * y + 7ll * f) & 63) - 32 + (int)(h & 15u);
+                v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            }
+            w[i >> 2] |= (uint32_t)v << (8 * (i & 3));
+        }
+        if (base + 16 <= n_pix) {
+            *(uint4*)(out + base) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+            for (int i = 0; base + i < n_pix; i++) out[base + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        }
+    }
+}
+
+// =============================================================================================
+// Launchers
+// =============================================================================================
+int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
+    const uint32_t groups = (uint32_t)((P.n_cubes + kCubesPerWave * kWavesPerBlock - 1) / (kCubesPerWave * kWavesPerBlock));
+    if (groups == 0) return 0;
+    if (D == 8) hipLaunchKernelGGL(encode_kernel<8>, dim3(groups), dim3(kBlock), 0, st, P);
+    else hipLaunchKernelGGL(encode_kernel<4>, dim3(groups), dim3(kBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st) {
+    if (D == 8) hipLaunchKernelGGL(encode_fixup_kernel<8>, dim3(grid), dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(encode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
+    const uint32_t groups = (uint32_t)((P.n_cubes + kCubesPerWave * kWavesPerBlock - 1) / (kCubesPerWave * kWavesPerBlock));
+    if (groups == 0) return 0;
+    if (D == 8) hipLaunchKernelGGL(decode_kernel<8>, dim3(groups), dim3(kBlock), 0, st, P);
+    else hipLaunchKernelGGL(decode_kernel<4>, dim3(groups), dim3(kBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st) {
+    if (D == 8) hipLaunchKernelGGL(decode_fixup_kernel<8>, dim3(grid), dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(decode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,
+                 hipStream_t st) {
+    long long chunks = (n_pix + 15) / 16;
+    long long blocks = (chunks + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, width, height, n_pix, seed,
+                       frame0, kind);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace dct3d

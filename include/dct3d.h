@@ -1,0 +1,144 @@
+/*
+ * dct3d.h -- C-ABI of the MI355X 3D-DCT hot path (libdct3d.so).
+ *
+ * Drop-in boundary for julianopiccoli/3dDCTVideoEncoding's per-stack device block.  The reference
+ * C codec (3d-DCT-video-encoding-OpenCL/) does, per 8-frame stack:
+ *     readCubes -> clEnqueueWriteBuffer -> dct_calculate_partial_sums -> dct_aggregate_partial_sums
+ *     -> clEnqueueReadBuffer -> applyQuantization                       (encoder.c:228-282)
+ *     applyDequantization -> clEnqueueWriteBuffer -> idct_calculate_partial_sums
+ *     -> idct_aggregate_partial_sums -> clEnqueueReadBuffer -> writeCubes (decoder.c:246-295)
+ * after a per-call OpenCL setup (encoder.c:169-219, decoder.c:153-202, OpenCLUtils.c:49-165).
+ * Each entry point below names the reference region it replaces.
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes, no framework types; 0 = DCT3D_OK, non-zero = DCT3D_E* code
+ *     (the reference printf()s and returns 1, or exit(1)s inside OpenCLUtils.c; this library never
+ *     prints and never exits -- the codec layer above prints, see codec.h);
+ *   - a context owns its device buffers and its HIP stream (the reference creates its OpenCL objects
+ *     per call and never releases them, encoder.c:187-219); one context per device, one host
+ *     thread per context (a context is not thread-safe);
+ *   - host-pointer entry points are synchronous on return (the reference's blocking
+ *     clEnqueueWrite/ReadBuffer, encoder.c:231,276); *_dev entry points take device pointers and
+ *     are asynchronous on the context stream (use dct3d_synchronize);
+ *   - frame width must be a multiple of the block width and height of the block height
+ *     (1080 = 135 * 8); the reference silently overruns otherwise, this library returns
+ *     DCT3D_EINVAL.
+ *
+ * Layouts:
+ *   raster  : u8 frames, frame-major, row-major (the raw grayscale file format, encoder.c:43-49);
+ *             a "stack" is DCT_BLOCK_DEPTH consecutive frames.
+ *   cubes   : cube-major: for each stack, block-row by, block-col bx, then (z, y, x) inside the cube
+ *             (readCubes order, encoder.c:51-63; Java Encoder.java:75-89).
+ *
+ * Numerics (parity target = the reference Java codec, BASELINE.json north_star):
+ *   - dct3d_encode_stacks*: quantised int32 coefficients equal to the Java path
+ *       Math.round(DCT.apply(...)[k] / max(1, 5(x+y+z)))          (Encoder.java:82, DCT.java:41-59)
+ *     bit for bit: computed in fp32 under a rigorous per-coefficient error bound; any coefficient
+ *     whose quotient is within that bound of a rounding tie is recomputed by replaying the Java
+ *     fold exactly (fp64, HashMap group order), and the DC from the exact integer cube sum.
+ *   - dct3d_decode_stacks*: u8 pixels equal to the Java path (byte) clamp(InverseDCT(...))
+ *     (InverseDCT.java:33-82, Decoder.java:112) bit for bit, same certify-or-replay scheme (fp64).
+ *   - float outputs (dct_opt, dct3d_forward_f32, dct3d_inverse_f32): fp64 internal arithmetic;
+ *     |err| <= 1e-9 * max(1, |value|) before the final rounding to the output type.
+ */
+#ifndef DCT3D_H_
+#define DCT3D_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCT3D_OK 0
+#define DCT3D_EINVAL 1      /* bad argument / unsupported block dims / misaligned frame size */
+#define DCT3D_EDEVICE 2     /* no such HIP device, or a HIP runtime error */
+#define DCT3D_ENOMEM 3      /* device or host allocation failed */
+#define DCT3D_EKERNEL 4     /* a kernel launch failed */
+
+#define DCT3D_ABI_VERSION 1
+
+typedef struct dct3d_ctx dct3d_ctx;
+
+/* Per-call statistics of the certify-or-replay scheme (last encode/decode call on the ctx). */
+typedef struct {
+    uint64_t n_units;          /* coefficients (encode) or pixels (decode) produced by the last call */
+    uint64_t n_flagged;        /* units of the last call re-done by the exact Java fold */
+    uint64_t n_overflow_cubes; /* cubes of the last call fully re-done because the flag list was full */
+    /* HIP-event timing of every encode/decode call since dct3d_reset_timers (profiling on) */
+    uint64_t n_timed;          /* calls timed */
+    double kernel_ms_total;    /* main transform kernel, summed */
+    double fixup_ms_total;     /* exact-fold kernel, summed */
+} dct3d_stats;
+
+/* ABI version of the loaded library (DCT3D_ABI_VERSION). */
+int dct3d_abi_version(void);
+const char *dct3d_strerror(int code);
+
+/* Replaces the per-call OpenCL setup: getDeviceId/getMaxWorkGroupSize (OpenCLUtils.c:69-104),
+ * clCreateContext/buildKernel/clCreateBuffer/clCreateCommandQueue/clCreateKernel
+ * (encoder.c:180-219, decoder.c:163-202).  `device` is a 0-based HIP ordinal (the codec layer
+ * maps the reference's 1-based platformIndex, main.c:33-37).  Block dims are the codec.h macros
+ * DCT_BLOCK_WIDTH/HEIGHT/DEPTH (codec.h:11-13); supported: 8 x 8 x 8 and 8 x 8 x 4. */
+int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ctx **out);
+void dct3d_ctx_destroy(dct3d_ctx *ctx);
+
+/* Use an external hipStream_t (e.g. a framework's current stream) instead of the ctx-owned one.
+ * NULL restores the ctx-owned stream. */
+int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
+/* Enable HIP-event timing of the kernels (reported by dct3d_get_stats). */
+int dct3d_ctx_set_profiling(dct3d_ctx *ctx, int on);
+int dct3d_synchronize(dct3d_ctx *ctx);
+/* Reads back the device counters of the last encode/decode and resolves the timing events
+ * (synchronises the stream). */
+int dct3d_get_stats(dct3d_ctx *ctx, dct3d_stats *out);
+int dct3d_reset_timers(dct3d_ctx *ctx);
+
+/* ---------------------------------------------------------------------------------------------
+ * Native fused path (B): replaces readCubes + H2D + dct kernels + D2H + applyQuantization
+ * (encoder.c:228-282) for n_stacks consecutive stacks.
+ *   raster : n_stacks * block_d frames of width*height u8
+ *   q_cubes: n_stacks * (width/bw) * (height/bh) cubes of bw*bh*bd int32 (cube-major)
+ *   dct_opt: optional (may be NULL) fp64 DCT coefficients, same cube-major layout (the Java
+ *            dctCoeff values, Encoder.java:66, for the float-DCT parity check)
+ * ------------------------------------------------------------------------------------------- */
+int dct3d_encode_stacks(dct3d_ctx *ctx, const uint8_t *raster, int width, int height, int n_stacks,
+                        int32_t *q_cubes, double *dct_opt);
+int dct3d_encode_stacks_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height,
+                            int n_stacks, int32_t *d_q_cubes, double *d_dct_opt);
+
+/* Replaces applyDequantization + H2D + idct kernels + D2H + writeCubes (decoder.c:246-295). */
+int dct3d_decode_stacks(dct3d_ctx *ctx, const int32_t *q_cubes, int width, int height, int n_stacks,
+                        uint8_t *raster);
+int dct3d_decode_stacks_dev(dct3d_ctx *ctx, const int32_t *d_q_cubes, int width, int height,
+                            int n_stacks, uint8_t *d_raster);
+
+/* ---------------------------------------------------------------------------------------------
+ * Reference-faithful drop-in (A): the exact data flow of the OpenCL block, float cube-major in,
+ * float cube-major out (kernelInputData -> kernelOutputData, encoder.c:187-276 / decoder.c:
+ * 170-292).  The caller keeps readCubes/applyQuantization (forward) and applyDequantization/
+ * writeCubes (inverse) on the host, exactly as the reference does.
+ *   dct3d_forward_f32: orthonormal 3D DCT-II of each cube (dct_* kernels, 3dDCT.cl:43-143)
+ *   dct3d_inverse_f32: 3D inverse DCT clamped to [0,255] (idct_* kernels, 3dDCT.cl:164-265)
+ * ------------------------------------------------------------------------------------------- */
+int dct3d_forward_f32(dct3d_ctx *ctx, const float *cubes, size_t n_cubes, float *coeffs);
+int dct3d_inverse_f32(dct3d_ctx *ctx, const float *coeffs, size_t n_cubes, float *pixels);
+int dct3d_forward_f32_dev(dct3d_ctx *ctx, const float *d_cubes, size_t n_cubes, float *d_coeffs);
+int dct3d_inverse_f32_dev(dct3d_ctx *ctx, const float *d_coeffs, size_t n_cubes, float *d_pixels);
+
+/* ---------------------------------------------------------------------------------------------
+ * Benchmark / test support: integer-only deterministic synthetic frames, identical to the
+ * Python generator (3ddctvideoencoding_amd.synthetic).  For global pixel index
+ * idx = ((frame0 + f) * height + y) * width + x:
+ *   kind 0 ("ramp"):    clamp(128 + ((3x + 5y + 7(frame0+f)) & 63) - 32 + (splitmix64(seed ^ idx) & 15))
+ *   kind 1 ("uniform"): splitmix64(seed ^ idx) & 255
+ * ------------------------------------------------------------------------------------------- */
+int dct3d_fill_synthetic_dev(dct3d_ctx *ctx, uint8_t *d_frames, int width, int height, int n_frames,
+                             uint64_t seed, int64_t frame0, int kind);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DCT3D_H_ */
