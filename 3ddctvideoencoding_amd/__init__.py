@@ -62,6 +62,13 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build())")
+        # PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7).  If libdct3d.so were
+        # loaded first, torch would later load a second HIP runtime and find no GPU; loading torch
+        # first lets libdct3d.so bind to the already-loaded runtime (one HIP runtime per process).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         vp, i32, sz, u64, i64 = C.c_void_p, C.c_int, C.c_size_t, C.c_uint64, C.c_int64
         L.dct3d_abi_version.restype = i32
