@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "dct_butterfly.h"
 #include "dct3d_kernels.h"
@@ -92,21 +93,34 @@ __device__ __forceinline__ void load_rows(const EncodeParams& P, uint32_t g, boo
     }
 }
 
-// Cube statistics over the 8 lanes of a cube: S = sum, m = integer mean, A = max |x - m|.
 template <int D>
-__device__ __forceinline__ void cube_stats(const uint2 (&raw)[D], uint32_t& S, int& m, float& A) {
+__device__ __forceinline__ void to_float(const uint2 (&raw)[D], float (&a)[D][8]) {
+#pragma unroll
+    for (int z = 0; z < D; z++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            a[z][e] = byte_of(raw[z].x, e);
+            a[z][e + 4] = byte_of(raw[z].y, e);
+        }
+}
+
+// Cube statistics over the 8 lanes of a cube: S = sum, m = integer mean, A = max |x - m|.
+// min/max on the float bit patterns (non-negative floats order like integers): v_max3/v_min3_u32.
+template <int D>
+__device__ __forceinline__ void cube_stats(const uint2 (&raw)[D], const float (&a)[D][8], uint32_t& S, int& m,
+                                           float& A) {
     constexpr int CS = 64 * D;
     S = 0;
-    uint32_t mx = 0, mn = 255;
+    uint32_t mx = 0u, mn = 0x7F800000u;
 #pragma unroll
     for (int z = 0; z < D; z++) {
         S = __builtin_amdgcn_udot4(raw[z].x, 0x01010101u, S, false);
         S = __builtin_amdgcn_udot4(raw[z].y, 0x01010101u, S, false);
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint32_t v0 = (raw[z].x >> (8 * b)) & 0xFFu, v1 = (raw[z].y >> (8 * b)) & 0xFFu;
-            mx = max(mx, max(v0, v1));
-            mn = min(mn, min(v0, v1));
+        for (int x = 0; x < 8; x += 2) {
+            const uint32_t u0 = __float_as_uint(a[z][x]), u1 = __float_as_uint(a[z][x + 1]);
+            mx = max(mx, max(u0, u1));
+            mn = min(mn, min(u0, u1));
         }
     }
 #pragma unroll
@@ -116,21 +130,14 @@ __device__ __forceinline__ void cube_stats(const uint2 (&raw)[D], uint32_t& S, i
         mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
     }
     m = (int)((S + CS / 2) / CS);
-    A = (float)max((int)mx - m, m - (int)mn);
+    const float mf = (float)m;
+    A = fmaxf(__uint_as_float(mx) - mf, mf - __uint_as_float(mn));  // exact (small integers)
 }
 
-// Full forward transform of the wave's 8 cubes: row layout -> face layout coefficients b[ky][kx'].
+// Forward transform of the wave's 8 cubes: row layout a[z][x] -> face layout coefficients b[ky][kx'].
 // Uses the wave's LDS region (no cross-wave sharing).
 template <int D, int NB>
-__device__ __forceinline__ void forward_cube(const uint2 (&raw)[D], int m, int c, int j, char* wl, float (&b)[8][NB]) {
-    float a[D][8];
-#pragma unroll
-    for (int z = 0; z < D; z++)
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            a[z][e] = byte_of(raw[z].x, e);
-            a[z][e + 4] = byte_of(raw[z].y, e);
-        }
+__device__ __forceinline__ void forward_cube(float (&a)[D][8], int m, int c, int j, char* wl, float (&b)[8][NB]) {
     const float dcsub = 8.0f * (float)m;
     // pass X (integer front exact, cube-mean centring folded into X0), pass Z
 #pragma unroll
@@ -195,8 +202,21 @@ __device__ __forceinline__ void forward_cube(const uint2 (&raw)[D], int m, int c
     }
 }
 
-template <int D>
-__global__ __launch_bounds__(kBlock) void encode_kernel(EncodeParams P) {
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ void store16(void* p, const int4& v) {
+    if constexpr (NT) {
+        i32x4_t t = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(t, (i32x4_t*)p);
+    } else {
+        *(int4*)p = v;
+    }
+}
+
+// One wave = ITER consecutive groups of 8 cubes; the rows of group it+1 are loaded (16 VGPRs)
+// before group it is transformed, so every wave keeps loads in flight while it computes.
+template <int D, int ITER, bool NT>
+__global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(EncodeParams P) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
     constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
@@ -205,118 +225,141 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(EncodeParams P) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = lane >> 3, j = lane & 7;
     char* wl = lds + wave * kWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
-    const uint32_t g = cube0 + c;
-    const bool valid = g < P.n_cubes;
+    const uint32_t group0 = (blockIdx.x * kWavesPerBlock + wave) * ITER;
 
-    uint2 raw[D];
-    load_rows<D>(P, g, valid, j, raw);
-    uint32_t S;
-    int m;
-    float A;
-    cube_stats<D>(raw, S, m, A);
-    asm volatile("" : "+v"(S), "+v"(m), "+v"(A));  // compute the stats now: raw dies after conversion
-
-    float b[8][NB];
-    forward_cube<D, NB>(raw, m, c, j, wl, b);
-
-    // ---- quantise + certify (in place: b becomes the integer coefficients) ----
     const int kz = (D == 8) ? j : (j >> 1);
     const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
     const int so = kz + kx0;
-    float rr[NI], thr[NI];
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-        rr[i] = P.tab_rstep[so + i];
-        thr[i] = __builtin_fmaf(-A, P.tab_G[so + i], 0.5f - P.tab_E[so + i]);
-    }
-    int32_t qv[8][NB];
-    int flag = 0;
-#pragma unroll
-    for (int ky = 0; ky < 8; ky++) {
-        pin(b[ky]);
-        bool f = false;
-#pragma unroll
-        for (int x = 0; x < NB; x++) {
-            const float q = b[ky][x] * rr[ky + x];
-            const float n = __builtin_rintf(q);
-            f |= __builtin_fabsf(q - n) >= thr[ky + x];
-            qv[ky][x] = (int32_t)n;
-        }
-        flag |= (int)f;
-        pin(qv[ky]);
-        asm volatile("" : "+v"(flag));  // the row's checks complete here (q, n die)
-    }
-    if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
 
-    // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
-    constexpr int ROUNDS = (D == 8) ? 2 : 1;
-    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
-#pragma unroll
-    for (int rd = 0; rd < ROUNDS; rd++) {
-        if ((c / CUBES_PER_ROUND) == rd) {
-            const int cc = c % CUBES_PER_ROUND;
-            if constexpr (D == 8) {
-#pragma unroll
-                for (int ky = 0; ky < 8; ky++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++)
-                        *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
-                            make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
-            } else {
-#pragma unroll
-                for (int ky = 0; ky < 8; ky++)
-                    *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
-                        make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
-            }
-        }
-        wave_lds_sync();
-        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
-        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
-            const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
-            const int face = (q >> 4) % D;
-            const int w = q & 15;
-            if (rcube0 + cc < P.n_cubes) {
-                const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
-                *(int4*)(outb + (size_t)q * 16) = v;
-            }
-        }
-        wave_lds_sync();
-    }
+    uint2 rawn[D];
+    load_rows<D>(P, group0 * kCubesPerWave + c, group0 * kCubesPerWave + c < P.n_cubes, j, rawn);
 
-    // ---- rare path: identify uncertified coefficients (recomputed from the raw rows) ----
-    if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
-        uint2 raw2[D];
-        load_rows<D>(P, g, valid, j, raw2);  // reload (rare path) instead of keeping 2*D VGPRs live
-        float b2[8][NB];
-        forward_cube<D, NB>(raw2, m, c, j, wl, b2);
-        bool overflow = false;
-        if (flag && valid) {
+#pragma unroll 1
+    for (int it = 0; it < ITER; it++) {
+        const uint32_t cube0 = (group0 + it) * kCubesPerWave;
+        if (cube0 >= P.n_cubes) break;  // wave-uniform
+        const uint32_t g = cube0 + c;
+        const bool valid = g < P.n_cubes;
+        uint2 raw[D];
 #pragma unroll
-            for (int ky = 0; ky < 8; ky++)
+        for (int z = 0; z < D; z++) raw[z] = rawn[z];
+        if (it + 1 < ITER) {
+            const uint32_t gn = cube0 + kCubesPerWave + c;
+            load_rows<D>(P, gn, gn < P.n_cubes, j, rawn);  // prefetch the next group
+        }
+
+        float a[D][8];
+        to_float<D>(raw, a);
+        uint32_t S;
+        int m;
+        float A;
+        cube_stats<D>(raw, a, S, m, A);
+        asm volatile("" : "+v"(S), "+v"(m), "+v"(A));  // stats now: raw dies after conversion
+
+        float b[8][NB];
+        forward_cube<D, NB>(a, m, c, j, wl, b);
+
+        // ---- quantise + certify (thr_s = 0.5 - (A*G_s + E_s), dct3d_plan.cpp) ----
+        // The per-lane tables are re-read each iteration (an opaque zero keeps the compiler from
+        // hoisting ~45 loop-invariant registers out of the loop; the reads hit L1/L2).
+        int sz = so;
+        asm volatile("" : "+v"(sz));
+        float rr[NI], thr[NI];
 #pragma unroll
-                for (int x = 0; x < NB; x++) {
-                    const float rr2 = P.tab_rstep[so + ky + x];
-                    const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
-                    const float q = b2[ky][x] * rr2;
-                    const float n = __builtin_rintf(q);
-                    if (__builtin_fabsf(q - n) >= th2) {
-                        const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
-                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
-                        else overflow = true;
-                    }
+        for (int i = 0; i < NI; i++) {
+            rr[i] = P.tab_rstep[sz + i];
+            thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
+        }
+        int32_t qv[8][NB];
+        int flag = 0;
+#pragma unroll
+        for (int ky = 0; ky < 8; ky++) {
+            pin(b[ky]);
+            bool f = false;
+#pragma unroll
+            for (int x = 0; x < NB; x++) {
+                const float q = b[ky][x] * rr[ky + x];
+                const float n = __builtin_rintf(q);
+                f |= __builtin_fabsf(q - n) >= thr[ky + x];
+                qv[ky][x] = (int32_t)n;
+            }
+            flag |= (int)f;
+            pin(qv[ky]);
+            asm volatile("" : "+v"(flag));  // the row's checks complete here (q, n die)
+        }
+        if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+
+        // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
+        constexpr int ROUNDS = (D == 8) ? 2 : 1;
+        constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
+#pragma unroll
+        for (int rd = 0; rd < ROUNDS; rd++) {
+            if ((c / CUBES_PER_ROUND) == rd) {
+                const int cc = c % CUBES_PER_ROUND;
+                if constexpr (D == 8) {
+#pragma unroll
+                    for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                        for (int h = 0; h < 2; h++)
+                            *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
+                                make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
+                } else {
+#pragma unroll
+                    for (int ky = 0; ky < 8; ky++)
+                        *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
+                            make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
                 }
+            }
+            wave_lds_sync();
+            const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
+            char* outb = (char*)(P.out + (size_t)rcube0 * CS);
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
+                const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
+                const int face = (q >> 4) % D;
+                const int w = q & 15;
+                if (rcube0 + cc < P.n_cubes) {
+                    const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
+                    store16<NT>(outb + (size_t)q * 16, v);
+                }
+            }
+            wave_lds_sync();
         }
-        // at most one cube-list entry per cube: the lowest overflowing lane of the cube appends
-        const unsigned long long ov = __ballot(overflow);
-        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
-        if (overflow && (__builtin_ctz(mine) == j)) {
-            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
+
+        // ---- rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
+        if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
+            uint2 raw2[D];
+            load_rows<D>(P, g, valid, j, raw2);
+            float a2[D][8];
+            to_float<D>(raw2, a2);
+            float b2[8][NB];
+            forward_cube<D, NB>(a2, m, c, j, wl, b2);
+            bool overflow = false;
+            if (flag && valid) {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                    for (int x = 0; x < NB; x++) {
+                        const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
+                        const float q = b2[ky][x] * rr[ky + x];
+                        const float n = __builtin_rintf(q);
+                        if (__builtin_fabsf(q - n) >= th2) {
+                            const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
+                            const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                            if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
+                            else overflow = true;
+                        }
+                    }
+            }
+            // at most one cube-list entry per cube: the lowest overflowing lane of the cube appends
+            const unsigned long long ov = __ballot(overflow);
+            const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
+            if (overflow && (__builtin_ctz(mine) == j)) {
+                const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+                P.cube_list[idx] = g;  // capacity n_cubes: never overflows
+            }
+            wave_lds_sync();
         }
     }
 }
@@ -631,11 +674,40 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, int width, int
 // =============================================================================================
 // Launchers
 // =============================================================================================
+// Encode variants (template <D, ITER, NT>): ITER = 8-cube groups per wave (register prefetch
+// pipeline depth along the wave's cubes), NT = non-temporal stores of the int32 output.
+// DCT3D_ENC_VARIANT (test/bench knob) selects one; default kDefaultVariant.
+namespace {
+constexpr int kDefaultVariant = 1;
+template <int D, int ITER, bool NT>
+void launch_enc_t(const EncodeParams& P, hipStream_t st) {
+    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
+    const uint32_t waves = (groups + ITER - 1) / ITER;
+    const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((encode_kernel<D, ITER, NT>), dim3(blocks), dim3(kBlock), 0, st, P);
+}
+template <int D>
+void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
+    switch (v) {
+        case 0: launch_enc_t<D, 1, false>(P, st); break;
+        case 1: launch_enc_t<D, 1, true>(P, st); break;
+        case 2: launch_enc_t<D, 4, false>(P, st); break;
+        case 3: launch_enc_t<D, 4, true>(P, st); break;
+        case 4: launch_enc_t<D, 16, false>(P, st); break;
+        default: launch_enc_t<D, 16, true>(P, st); break;
+    }
+}
+}  // namespace
+
 int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
-    const uint32_t groups = (uint32_t)((P.n_cubes + kCubesPerWave * kWavesPerBlock - 1) / (kCubesPerWave * kWavesPerBlock));
-    if (groups == 0) return 0;
-    if (D == 8) hipLaunchKernelGGL(encode_kernel<8>, dim3(groups), dim3(kBlock), 0, st, P);
-    else hipLaunchKernelGGL(encode_kernel<4>, dim3(groups), dim3(kBlock), 0, st, P);
+    if (P.n_cubes == 0) return 0;
+    static int variant = -1;
+    if (variant < 0) {
+        const char* e = getenv("DCT3D_ENC_VARIANT");
+        variant = e ? atoi(e) : kDefaultVariant;
+    }
+    if (D == 8) launch_enc_variant<8>(variant, P, st);
+    else launch_enc_variant<4>(variant, P, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
