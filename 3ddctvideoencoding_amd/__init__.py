@@ -35,7 +35,7 @@ ABI_SYMBOLS = (
     "dct3d_reset_timers",
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
-    "dct3d_fill_synthetic_dev",
+    "dct3d_fill_synthetic_dev", "dct3d_plan_query",
 )
 
 
@@ -43,6 +43,12 @@ class Dct3dError(RuntimeError):
     def __init__(self, code: int, what: str):
         super().__init__(f"{what}: {strerror(code)} ({code})")
         self.code = code
+
+
+class PlanInfo(C.Structure):
+    _fields_ = [("cube_size", C.c_int), ("n_mults", C.c_int), ("treeified", C.c_int), ("coef_dc", C.c_double),
+                ("dec_G", C.c_double), ("dec_E", C.c_double), ("enc_rstep", C.c_float * 32),
+                ("enc_G", C.c_float * 32), ("enc_E", C.c_float * 32)]
 
 
 class Stats(C.Structure):
@@ -89,6 +95,7 @@ def lib() -> C.CDLL:
         for name in ("dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev"):
             getattr(L, name).argtypes = [vp, vp, sz, vp]
         L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
+        L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -118,6 +125,23 @@ def _tptr(t) -> int:
     if not t.is_contiguous():
         raise ValueError("tensor must be contiguous")
     return t.data_ptr()
+
+
+def plan_query(block_w: int = 8, block_h: int = 8, block_d: int = 8) -> dict:
+    """Host-side transform plan (no device): Java fold tables + certification tables."""
+    cs = block_w * block_h * block_d
+    info = PlanInfo()
+    ng = np.empty(cs, np.int32)
+    coef = np.empty(cs * 64, np.float64)
+    gof = np.empty(cs * cs, np.uint8)
+    K = np.empty(cs, np.float64)
+    _check(lib().dct3d_plan_query(block_w, block_h, block_d, C.byref(info), _ptr(ng), _ptr(coef), _ptr(gof), _ptr(K)),
+           "dct3d_plan_query")
+    return {"cube_size": info.cube_size, "n_mults": info.n_mults, "treeified": bool(info.treeified),
+            "coef_dc": info.coef_dc, "dec_G": info.dec_G, "dec_E": info.dec_E,
+            "enc_rstep": np.array(info.enc_rstep[:]), "enc_G": np.array(info.enc_G[:]),
+            "enc_E": np.array(info.enc_E[:]), "ngroups": ng, "coef": coef.reshape(cs, 64),
+            "group_of": gof.reshape(cs, cs), "enc_K": K}
 
 
 class Context:

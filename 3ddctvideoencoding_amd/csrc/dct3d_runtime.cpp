@@ -87,6 +87,29 @@ static int upload(DevBuf& b, const void* src, size_t bytes) {
     return hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? DCT3D_OK : DCT3D_EDEVICE;
 }
 
+int dct3d_plan_query(int bw, int bh, int bd, dct3d_plan_info* info, int32_t* ngroups, double* coef,
+                     uint8_t* group_of, double* enc_K) {
+    Plan p;
+    if (!build_plan(bw, bh, bd, p)) return DCT3D_EINVAL;
+    if (info) {
+        memset(info, 0, sizeof(*info));
+        info->cube_size = p.cs;
+        info->n_mults = p.n_mults;
+        info->treeified = p.treeified ? 1 : 0;
+        info->coef_dc = p.coef_dc;
+        info->dec_G = p.dec_G;
+        info->dec_E = p.dec_E;
+        memcpy(info->enc_rstep, p.enc_rstep, sizeof(info->enc_rstep));
+        memcpy(info->enc_G, p.enc_G, sizeof(info->enc_G));
+        memcpy(info->enc_E, p.enc_E, sizeof(info->enc_E));
+    }
+    if (ngroups) memcpy(ngroups, p.fwd_ngroups.data(), sizeof(int32_t) * p.cs);
+    if (coef) memcpy(coef, p.fwd_coef.data(), sizeof(double) * p.fwd_coef.size());
+    if (group_of) memcpy(group_of, p.fwd_group_of.data(), p.fwd_group_of.size());
+    if (enc_K) memcpy(enc_K, p.enc_K.data(), sizeof(double) * p.cs);
+    return DCT3D_OK;
+}
+
 int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ctx** out) {
     if (!out) return DCT3D_EINVAL;
     *out = nullptr;

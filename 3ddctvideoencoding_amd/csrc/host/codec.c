@@ -1,0 +1,169 @@
+/* codec.c -- encode()/decode(): the reference codec's pipeline (encoder.c:110-315,
+ * decoder.c:85-314) with the OpenCL block replaced by the libdct3d C-ABI.
+ *
+ * encode: per batch of stacks: fread -> dct3d_encode_stacks (fused DCT + quantisation on the GPU,
+ *         Java semantics) -> per stack: diagonal order + Exp-Golomb + deflate (codec_entropy.c).
+ * decode: inflate + Exp-Golomb + reorder per stack -> dct3d_decode_stacks (fused dequantisation +
+ *         IDCT + clamp + truncation on the GPU) -> fwrite.
+ * A stack is DCT_BLOCK_DEPTH frames; a short last stack is zero-filled (the reference reads
+ * uninitialised bytes there, encoder.c:43-49).  Frames to encode are rounded up to whole stacks,
+ * as in the reference loop (encoder.c:225).  Errors: printf + return 1 (the reference convention);
+ * never exit(). */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "codec.h"
+#include "codec_entropy.h"
+#include "dct3d.h"
+
+static int default_batch(void) {
+    const char *e = getenv("DCT3D_CODEC_BATCH");
+    int b = e ? atoi(e) : 16;
+    return b > 0 ? b : 16;
+}
+
+int encode_ex(const char *inName, const char *outName, int width, int height, int frames, int platformIndex,
+              int depth, int batch) {
+    if (width <= 0 || height <= 0 || width % 8 || height % 8 || frames <= 0 || (depth != 8 && depth != 4)) {
+        printf("Invalid geometry: %dx%d, %d frames, block depth %d (width/height must be multiples of 8)\n", width,
+               height, frames, depth);
+        return 1;
+    }
+    if (batch <= 0) batch = default_batch();
+    FILE *in = fopen(inName, "rb");
+    if (!in) {
+        printf("Cannot open input file %s\n", inName);
+        return 1;
+    }
+    FILE *out = fopen(outName, "wb");
+    if (!out) {
+        printf("Cannot open output file %s\n", outName);
+        fclose(in);
+        return 1;
+    }
+    dct3d_ctx *ctx = NULL;
+    int rc = dct3d_ctx_create(platformIndex > 0 ? platformIndex - 1 : 0, 8, 8, depth, &ctx);
+    if (rc) {
+        printf("Error creating the device context: %s\n", dct3d_strerror(rc));
+        fclose(in);
+        fclose(out);
+        return 1;
+    }
+    const size_t frame = (size_t)width * height, stack_px = frame * depth;
+    const int n_stacks = (frames + depth - 1) / depth;
+    uint8_t *raster = (uint8_t *)malloc(stack_px * batch);
+    int32_t *q = (int32_t *)malloc(stack_px * batch * sizeof(int32_t));
+    dct3d_entropy_enc *ent = dct3d_entropy_enc_create(width, height, depth, out);
+    int status = 0;
+    if (!raster || !q || !ent) {
+        printf("Out of memory\n");
+        status = 1;
+    }
+    for (int s0 = 0; !status && s0 < n_stacks; s0 += batch) {
+        const int nb = (n_stacks - s0) < batch ? (n_stacks - s0) : batch;
+        size_t got = 0, r;
+        const size_t want = stack_px * nb;
+        while (got < want && (r = fread(raster + got, 1, want - got, in)) > 0) got += r;
+        if (got < want) memset(raster + got, 0, want - got);
+        rc = dct3d_encode_stacks(ctx, raster, width, height, nb, q, NULL);
+        if (rc) {
+            printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
+            status = 1;
+            break;
+        }
+        for (int s = 0; s < nb; s++) {
+            if (dct3d_entropy_enc_push(ent, q + stack_px * s, s0 + s == n_stacks - 1)) {
+                printf("Error in the entropy coder\n");
+                status = 1;
+                break;
+            }
+            printf("Frames processed: %d\n", (s0 + s + 1) * depth);
+        }
+    }
+    dct3d_entropy_enc_destroy(ent);
+    free(raster);
+    free(q);
+    dct3d_ctx_destroy(ctx);
+    fclose(in);
+    if (fflush(out) || fclose(out)) status = 1;
+    if (!status) printf("Encoding process completed\n");
+    return status;
+}
+
+int decode_ex(const char *inName, const char *outName, int width, int height, int frames, int platformIndex,
+              int depth, int batch) {
+    if (width <= 0 || height <= 0 || width % 8 || height % 8 || frames <= 0 || (depth != 8 && depth != 4)) {
+        printf("Invalid geometry: %dx%d, %d frames, block depth %d\n", width, height, frames, depth);
+        return 1;
+    }
+    if (batch <= 0) batch = default_batch();
+    FILE *in = fopen(inName, "rb");
+    if (!in) {
+        printf("Cannot open input file %s\n", inName);
+        return 1;
+    }
+    FILE *out = fopen(outName, "wb");
+    if (!out) {
+        printf("Cannot open output file %s\n", outName);
+        fclose(in);
+        return 1;
+    }
+    dct3d_ctx *ctx = NULL;
+    int rc = dct3d_ctx_create(platformIndex > 0 ? platformIndex - 1 : 0, 8, 8, depth, &ctx);
+    if (rc) {
+        printf("Error creating the device context: %s\n", dct3d_strerror(rc));
+        fclose(in);
+        fclose(out);
+        return 1;
+    }
+    const size_t frame = (size_t)width * height, stack_px = frame * depth;
+    const int n_stacks = (frames + depth - 1) / depth;
+    uint8_t *raster = (uint8_t *)malloc(stack_px * batch);
+    int32_t *q = (int32_t *)malloc(stack_px * batch * sizeof(int32_t));
+    dct3d_entropy_dec *ent = dct3d_entropy_dec_create(width, height, depth, in, NULL, 0);
+    int status = 0;
+    if (!raster || !q || !ent) {
+        printf("Out of memory\n");
+        status = 1;
+    }
+    for (int s0 = 0; !status && s0 < n_stacks; s0 += batch) {
+        const int nb = (n_stacks - s0) < batch ? (n_stacks - s0) : batch;
+        for (int s = 0; s < nb; s++)
+            if (dct3d_entropy_dec_pull(ent, q + stack_px * s)) {
+                printf("Truncated or corrupt input stream\n");
+                status = 1;
+                break;
+            }
+        if (status) break;
+        rc = dct3d_decode_stacks(ctx, q, width, height, nb, raster);
+        if (rc) {
+            printf("Error running the inverse 3D DCT: %s\n", dct3d_strerror(rc));
+            status = 1;
+            break;
+        }
+        if (fwrite(raster, 1, stack_px * nb, out) != stack_px * nb) {
+            printf("Error writing the output file\n");
+            status = 1;
+            break;
+        }
+        printf("Frames processed: %d\n", (s0 + nb) * depth);
+    }
+    dct3d_entropy_dec_destroy(ent);
+    free(raster);
+    free(q);
+    dct3d_ctx_destroy(ctx);
+    fclose(in);
+    if (fflush(out) || fclose(out)) status = 1;
+    if (!status) printf("Decoding process completed\n");
+    return status;
+}
+
+int encode(char *inName, char *outName, int width, int height, int frames, int platformIndex) {
+    return encode_ex(inName, outName, width, height, frames, platformIndex, DCT_BLOCK_DEPTH, 0);
+}
+
+int decode(char *inName, char *outName, int width, int height, int frames, int platformIndex) {
+    return decode_ex(inName, outName, width, height, frames, platformIndex, DCT_BLOCK_DEPTH, 0);
+}

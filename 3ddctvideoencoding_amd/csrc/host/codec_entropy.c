@@ -1,0 +1,255 @@
+/* codec_entropy.c -- see codec_entropy.h. */
+#include "codec_entropy.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+#include "cube_utils.h"
+#include "exp_golomb.h"
+
+struct dct3d_entropy_enc {
+    z_stream zs;
+    FILE *out;
+    unsigned char *mem;
+    size_t mem_len, mem_cap;
+    char *eg;
+    size_t eg_cap;
+    struct ExpGolombStream st;
+    unsigned char zbuf[1 << 16];
+    struct SlicesPositions *sp;
+    int cs;
+    size_t cubes;       /* cubes per stack */
+    int finished;
+};
+
+static int sink(dct3d_entropy_enc *e, const unsigned char *p, size_t n) {
+    if (!n) return 0;
+    if (e->out) return fwrite(p, 1, n, e->out) == n ? 0 : -1;
+    if (e->mem_len + n > e->mem_cap) {
+        size_t cap = e->mem_cap ? e->mem_cap : 1 << 16;
+        while (cap < e->mem_len + n) cap *= 2;
+        unsigned char *m = (unsigned char *)realloc(e->mem, cap);
+        if (!m) return -1;
+        e->mem = m;
+        e->mem_cap = cap;
+    }
+    memcpy(e->mem + e->mem_len, p, n);
+    e->mem_len += n;
+    return 0;
+}
+
+static int deflate_all(dct3d_entropy_enc *e, const unsigned char *in, size_t n, int flush) {
+    e->zs.next_in = (Bytef *)in;
+    e->zs.avail_in = (uInt)n;
+    for (;;) {
+        e->zs.next_out = e->zbuf;
+        e->zs.avail_out = sizeof(e->zbuf);
+        int rc = deflate(&e->zs, flush);
+        if (rc == Z_STREAM_ERROR) return -1;
+        if (sink(e, e->zbuf, sizeof(e->zbuf) - e->zs.avail_out)) return -1;
+        if (flush == Z_FINISH) {
+            if (rc == Z_STREAM_END) return 0;
+        } else if (e->zs.avail_in == 0 && e->zs.avail_out != 0) {
+            return 0;
+        }
+    }
+}
+
+dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FILE *out) {
+    if (width <= 0 || height <= 0 || width % 8 || height % 8 || (depth != 8 && depth != 4)) return NULL;
+    dct3d_entropy_enc *e = (dct3d_entropy_enc *)calloc(1, sizeof(*e));
+    if (!e) return NULL;
+    e->out = out;
+    e->cs = 64 * depth;
+    e->cubes = (size_t)(width / 8) * (height / 8);
+    e->sp = cubeUtils_diagonalSlices(8, 8, depth);
+    /* worst case: 63 bits per value (|v| < 2^31) -> 8 bytes per value */
+    e->eg_cap = e->cubes * e->cs * 8 + 16;
+    e->eg = (char *)calloc(e->eg_cap, 1);
+    if (!e->sp || !e->eg || deflateInit(&e->zs, Z_BEST_COMPRESSION) != Z_OK) {  /* encoder.c:158-161 */
+        cubeUtils_deallocatePositions(e->sp);
+        free(e->eg);
+        free(e);
+        return NULL;
+    }
+    e->st.buffer = e->eg;
+    e->st.bitPosition = 8;
+    e->st.bufferPosition = 0;
+    return e;
+}
+
+int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last) {
+    if (e->finished) return -1;
+    /* applyExpGolombCoding (encoder.c:82-93): diagonal order inside each cube */
+    for (size_t c = 0; c < e->cubes; c++) {
+        const int32_t *cube = q + c * e->cs;
+        for (int i = 0; i < e->sp->length; i++) {
+            const struct ThreeDimensionalCoordinates p = e->sp->positions[i];
+            expGolomb_writeValue(&e->st, cube[p.x + p.y * 8 + p.z * 64]);
+        }
+    }
+    const int size = e->st.bufferPosition;
+    if (!is_last) {
+        if (deflate_all(e, (const unsigned char *)e->eg, (size_t)size, Z_NO_FLUSH)) return -1;
+        expGolomb_freeBuffer(&e->st, size, 1);  /* keep the partial byte (encoder.c:290) */
+        return 0;
+    }
+    e->finished = 1;
+    return deflate_all(e, (const unsigned char *)e->eg, (size_t)size + 1, Z_FINISH);  /* encoder.c:292 */
+}
+
+const unsigned char *dct3d_entropy_enc_memory(const dct3d_entropy_enc *e, size_t *len) {
+    if (len) *len = e->mem_len;
+    return e->mem;
+}
+
+void dct3d_entropy_enc_destroy(dct3d_entropy_enc *e) {
+    if (!e) return;
+    deflateEnd(&e->zs);
+    cubeUtils_deallocatePositions(e->sp);
+    free(e->eg);
+    free(e->mem);
+    free(e);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+struct dct3d_entropy_dec {
+    z_stream zs;
+    FILE *in;
+    const unsigned char *mem;
+    size_t mem_len, mem_pos;
+    int zeof, ieof;
+    unsigned char *buf;   /* inflated, unconsumed bytes */
+    size_t len, cap;
+    struct ExpGolombStream st;
+    unsigned char ibuf[1 << 16];
+    struct SlicesPositions *sp;
+    int cs;
+    size_t cubes;
+};
+
+dct3d_entropy_dec *dct3d_entropy_dec_create(int width, int height, int depth, FILE *in, const unsigned char *mem,
+                                            size_t len) {
+    if (width <= 0 || height <= 0 || width % 8 || height % 8 || (depth != 8 && depth != 4)) return NULL;
+    dct3d_entropy_dec *d = (dct3d_entropy_dec *)calloc(1, sizeof(*d));
+    if (!d) return NULL;
+    d->in = in;
+    d->mem = mem;
+    d->mem_len = len;
+    d->cs = 64 * depth;
+    d->cubes = (size_t)(width / 8) * (height / 8);
+    d->sp = cubeUtils_diagonalSlices(8, 8, depth);
+    d->cap = 1 << 20;
+    d->buf = (unsigned char *)malloc(d->cap);
+    if (!d->sp || !d->buf || inflateInit(&d->zs) != Z_OK) {
+        cubeUtils_deallocatePositions(d->sp);
+        free(d->buf);
+        free(d);
+        return NULL;
+    }
+    d->st.buffer = (char *)d->buf;
+    d->st.bitPosition = 8;
+    d->st.bufferPosition = 0;
+    return d;
+}
+
+/* make at least `need` unconsumed bytes available (or hit the end of the stream) */
+static int refill(dct3d_entropy_dec *d, size_t need) {
+    for (;;) {
+        const size_t avail = d->len - (size_t)d->st.bufferPosition;
+        if (avail >= need || d->zeof) return 0;
+        /* compact: drop consumed bytes (decoder.c:233-235) */
+        if (d->st.bufferPosition > 0) {
+            memmove(d->buf, d->buf + d->st.bufferPosition, avail);
+            d->len = avail;
+            d->st.bufferPosition = 0;
+        }
+        if (d->cap - d->len < (1 << 16)) {
+            unsigned char *b = (unsigned char *)realloc(d->buf, d->cap * 2);
+            if (!b) return -1;
+            d->buf = b;
+            d->cap *= 2;
+            d->st.buffer = (char *)b;
+        }
+        if (d->zs.avail_in == 0 && !d->ieof) {
+            if (d->in) {
+                size_t r = fread(d->ibuf, 1, sizeof(d->ibuf), d->in);
+                if (r == 0) d->ieof = 1;
+                d->zs.next_in = d->ibuf;
+                d->zs.avail_in = (uInt)r;
+            } else {
+                size_t r = d->mem_len - d->mem_pos;
+                if (r > (1u << 30)) r = 1u << 30;
+                if (r == 0) d->ieof = 1;
+                d->zs.next_in = (Bytef *)(d->mem + d->mem_pos);
+                d->zs.avail_in = (uInt)r;
+                d->mem_pos += r;
+            }
+        }
+        d->zs.next_out = d->buf + d->len;
+        d->zs.avail_out = (uInt)(d->cap - d->len);
+        const int rc = inflate(&d->zs, Z_NO_FLUSH);
+        d->len = d->cap - d->zs.avail_out;
+        if (rc == Z_STREAM_END) d->zeof = 1;
+        else if (rc != Z_OK && rc != Z_BUF_ERROR) return -1;
+        else if (rc == Z_BUF_ERROR && d->ieof) d->zeof = 1;  /* truncated input */
+    }
+}
+
+int dct3d_entropy_dec_pull(dct3d_entropy_dec *d, int32_t *q) {
+    for (size_t c = 0; c < d->cubes; c++) {
+        int32_t *cube = q + c * d->cs;
+        for (int i = 0; i < d->sp->length; i++) {
+            if (refill(d, 16)) return -1;
+            /* a codeword needs at most 8 bytes; past the end the stream is corrupt */
+            if (d->len - (size_t)d->st.bufferPosition < 9) {
+                if (d->len - (size_t)d->st.bufferPosition == 0) return -1;
+                memset(d->buf + d->len, 0xFF, 16 < d->cap - d->len ? 16 : d->cap - d->len);
+            }
+            const struct ThreeDimensionalCoordinates p = d->sp->positions[i];
+            cube[p.x + p.y * 8 + p.z * 64] = expGolomb_readValue(&d->st);
+            if ((size_t)d->st.bufferPosition > d->len) return -1;
+        }
+    }
+    return 0;
+}
+
+void dct3d_entropy_dec_destroy(dct3d_entropy_dec *d) {
+    if (!d) return;
+    inflateEnd(&d->zs);
+    cubeUtils_deallocatePositions(d->sp);
+    free(d->buf);
+    free(d);
+}
+
+int dct3d_codec_entropy_encode(const int32_t *q, int width, int height, int n_stacks, int depth, unsigned char **out,
+                               size_t *out_len) {
+    if (!out || !out_len || n_stacks <= 0) return -1;
+    dct3d_entropy_enc *e = dct3d_entropy_enc_create(width, height, depth, NULL);
+    if (!e) return -1;
+    const size_t per = e->cubes * (size_t)e->cs;
+    for (int s = 0; s < n_stacks; s++)
+        if (dct3d_entropy_enc_push(e, q + per * s, s == n_stacks - 1)) {
+            dct3d_entropy_enc_destroy(e);
+            return -1;
+        }
+    *out_len = e->mem_len;
+    *out = e->mem;
+    e->mem = NULL;
+    dct3d_entropy_enc_destroy(e);
+    return 0;
+}
+
+int dct3d_codec_entropy_decode(const unsigned char *bin, size_t len, int width, int height, int n_stacks, int depth,
+                               int32_t *q) {
+    dct3d_entropy_dec *d = dct3d_entropy_dec_create(width, height, depth, NULL, bin, len);
+    if (!d) return -1;
+    const size_t per = d->cubes * (size_t)d->cs;
+    int rc = 0;
+    for (int s = 0; s < n_stacks && !rc; s++) rc = dct3d_entropy_dec_pull(d, q + per * s);
+    dct3d_entropy_dec_destroy(d);
+    return rc;
+}
+
+void dct3d_codec_free(void *p) { free(p); }

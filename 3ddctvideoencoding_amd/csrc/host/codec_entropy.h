@@ -1,0 +1,45 @@
+/* codec_entropy.h -- the codec's entropy stage (diagonal-slice order -> signed Exp-Golomb -> zlib),
+ * stream-compatible with the reference C codec (encoder.c:82-108,263-296 / decoder.c:61-83,209-244):
+ * one zlib stream (Z_BEST_COMPRESSION); per stack deflate(Z_NO_FLUSH) of the complete Exp-Golomb
+ * bytes with the partial byte carried to the next stack; the last stack deflated with Z_FINISH
+ * including its partial byte (+1).  Internal to libdct3dcodec (exported for the tests). */
+#ifndef DCT3D_CODEC_ENTROPY_H_
+#define DCT3D_CODEC_ENTROPY_H_
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dct3d_entropy_enc dct3d_entropy_enc;
+typedef struct dct3d_entropy_dec dct3d_entropy_dec;
+
+/* sink: FILE* (out) or, if out == NULL, an internal growable memory buffer */
+dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FILE *out);
+/* q: one stack of cubes, cube-major int32; is_last selects Z_FINISH (encoder.c:288-293) */
+int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last);
+const unsigned char *dct3d_entropy_enc_memory(const dct3d_entropy_enc *e, size_t *len);
+void dct3d_entropy_enc_destroy(dct3d_entropy_enc *e);
+
+/* source: FILE* (in) or, if in == NULL, the memory block [mem, mem+len) */
+dct3d_entropy_dec *dct3d_entropy_dec_create(int width, int height, int depth, FILE *in, const unsigned char *mem,
+                                            size_t len);
+/* fills one stack of cubes (cube-major int32); returns 0, or -1 on a truncated/corrupt stream */
+int dct3d_entropy_dec_pull(dct3d_entropy_dec *d, int32_t *q);
+void dct3d_entropy_dec_destroy(dct3d_entropy_dec *d);
+
+/* whole-buffer helpers (tests): q = n_stacks stacks cube-major */
+int dct3d_codec_entropy_encode(const int32_t *q, int width, int height, int n_stacks, int depth,
+                               unsigned char **out, size_t *out_len);
+int dct3d_codec_entropy_decode(const unsigned char *bin, size_t len, int width, int height, int n_stacks, int depth,
+                               int32_t *q);
+void dct3d_codec_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -72,6 +72,27 @@ typedef struct {
     double fixup_ms_total;     /* exact-fold kernel, summed */
 } dct3d_stats;
 
+/* Transform-plan introspection (host only, no device needed). */
+typedef struct {
+    int cube_size;
+    int n_mults;          /* sum over coefficients of Java multiplication groups (11,567 for 8^3) */
+    int treeified;        /* 1 if Java's HashMap would have treeified a bin (fold order then unverified) */
+    double coef_dc;       /* the single DC group coefficient (DCT.java:110 with k = 0) */
+    double dec_G, dec_E;  /* decode certification: margin = max|coef| * dec_G + dec_E */
+    float enc_rstep[32];  /* encode certification per s = kx+ky+kz: fp32(1/max(1,5s)) */
+    float enc_G[32];      /*   threshold_s = 0.5 - (A * G_s + E_s), A = max|x - mean| of the cube */
+    float enc_E[32];
+} dct3d_plan_info;
+
+/* The plan for block dims (bw, bh, bd): the MI355X build's DCT.initialize (DCT.java:77-163) and
+ * InverseDCT.initialize (InverseDCT.java:87-133).  Optional arrays (NULL to skip), cs = bw*bh*bd:
+ *   ngroups [cs]       multiplication groups of each output coefficient k (fold length)
+ *   coef    [cs * 64]  group coefficients of k in Java HashMap iteration (fold) order
+ *   group_of[cs * cs]  fold index of input n in output k's fold (0xFF: dropped, key == 0)
+ *   enc_K   [cs]       fp32 rounding-error bound of coefficient k per unit max|x - mean| */
+int dct3d_plan_query(int bw, int bh, int bd, dct3d_plan_info *info, int32_t *ngroups, double *coef,
+                     uint8_t *group_of, double *enc_K);
+
 /* ABI version of the loaded library (DCT3D_ABI_VERSION). */
 int dct3d_abi_version(void);
 const char *dct3d_strerror(int code);

@@ -1,0 +1,75 @@
+"""CPU: the N>1 path -- contiguous stack sharding with no data-path collective, gloo world_size 2.
+
+Each rank encodes its own stack range with the Java-semantics oracle (the per-rank work stands in
+for the GPU kernel here), the shards are gathered to rank 0 in stack order and must equal the
+single-process encode; the timing reduction is max-over-ranks and the units are summed."""
+import importlib
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch.distributed as dist
+    import oracle
+    pkg = importlib.import_module("3ddctvideoencoding_amd")
+    sh = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    n_stacks = 5
+    first, count = sh.shard(n_stacks, world, rank)
+    frames = pkg.synthetic.frames(48, 32, count * 8, frame0=first * 8, kind="uniform")
+    q = oracle.Plan(8, 8, 8).encode_q(frames, threads=1) if count else np.zeros((0, 8, 8, 8), np.int32)
+    t, u = sh.reduce_timing(0.1 * (rank + 1), q.shape[0])
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object((first, q), parts, dst=0)
+    if rank == 0:
+        full = np.concatenate([p[1] for p in sorted(parts, key=lambda p: p[0])])
+        np.save(os.path.join(out_dir, "full.npy"), full)
+        np.save(os.path.join(out_dir, "tu.npy"), np.array([t, u]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_ranges():
+    sh = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    for n in (0, 1, 7, 64, 65):
+        for w in (1, 2, 3, 8):
+            rs = [sh.shard(n, w, r) for r in range(w)]
+            assert sum(c for _, c in rs) == n
+            assert all(rs[i][0] + rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            assert max(c for _, c in rs) - min(c for _, c in rs) <= 1
+    assert sh.shard(64, 8, 3) == (24, 8)   # config 4: 64 4K stacks over 8 GPUs
+    with pytest.raises(ValueError):
+        sh.shard(4, 2, 2)
+
+
+def test_world2_gloo_sharded_encode_equals_single(tmp_path, pkg, plan8):
+    mp.spawn(_worker, args=(2, _port(), str(tmp_path)), nprocs=2, join=True)
+    full = np.load(tmp_path / "full.npy")
+    frames = pkg.synthetic.frames(48, 32, 40, kind="uniform")
+    assert np.array_equal(full, plan8.encode_q(frames))
+    t, u = np.load(tmp_path / "tu.npy")
+    assert abs(t - 0.2) < 1e-12 and u == full.shape[0]
+
+
+def test_checksum_order_sensitive():
+    sh = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    a = np.arange(1000, dtype=np.int32)
+    assert sh.checksum(a) != sh.checksum(a[::-1].copy())
+    assert sh.checksum(a) == sh.checksum(a.copy())

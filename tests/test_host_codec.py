@@ -1,0 +1,222 @@
+"""CPU: the codec host layer (libdct3dcodec.so: cube_utils.c, exp_golomb.c, cube_io.c,
+codec_entropy.c) against the oracle and against the reference's own C helpers (oracle/_ref).
+
+The entropy stage (diagonal order -> Exp-Golomb -> zlib) is replayed with the reference encoder's
+own applyExpGolombCoding + applyZlibCompression + expGolomb_freeBuffer call sequence
+(encoder.c:263-296) and must produce the same .bin bytes.
+"""
+import ctypes as C
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+
+def codec(pkg):
+    pkg.lib()
+    L = C.CDLL(pkg.CODEC_LIB_PATH)
+    L.dct3d_codec_entropy_encode.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    L.dct3d_codec_entropy_decode.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.dct3d_codec_free.argtypes = [C.c_void_p]
+    return L
+
+
+class Coord(C.Structure):
+    _fields_ = [("x", C.c_int), ("y", C.c_int), ("z", C.c_int)]
+
+
+class Slices(C.Structure):
+    _fields_ = [("positions", C.POINTER(Coord)), ("length", C.c_int)]
+
+
+class EGStream(C.Structure):
+    _fields_ = [("buffer", C.c_void_p), ("bitPosition", C.c_int), ("bufferPosition", C.c_int)]
+
+
+class ZStream(C.Structure):  # zlib z_stream (LP64)
+    _fields_ = [("next_in", C.c_void_p), ("avail_in", C.c_uint), ("total_in", C.c_ulong),
+                ("next_out", C.c_void_p), ("avail_out", C.c_uint), ("total_out", C.c_ulong),
+                ("msg", C.c_char_p), ("state", C.c_void_p), ("zalloc", C.c_void_p), ("zfree", C.c_void_p),
+                ("opaque", C.c_void_p), ("data_type", C.c_int), ("adler", C.c_ulong), ("reserved", C.c_ulong)]
+
+
+def entropy_encode(pkg, q, w, h, stacks, depth):
+    L = codec(pkg)
+    out, n = C.c_void_p(), C.c_size_t()
+    q = np.ascontiguousarray(q, np.int32)
+    assert L.dct3d_codec_entropy_encode(q.ctypes.data, w, h, stacks, depth, C.byref(out), C.byref(n)) == 0
+    b = C.string_at(out, n.value)
+    L.dct3d_codec_free(out)
+    return b
+
+
+def entropy_decode(pkg, b, w, h, stacks, depth):
+    L = codec(pkg)
+    q = np.empty(stacks * w * h * depth, np.int32)
+    buf = C.create_string_buffer(b, len(b))
+    rc = L.dct3d_codec_entropy_decode(buf, len(b), w, h, stacks, depth, q.ctypes.data)
+    return rc, q
+
+
+def test_diagonal_slices_host(pkg, oracle):
+    L = codec(pkg)
+    L.cubeUtils_diagonalSlices.restype = C.POINTER(Slices)
+    L.cubeUtils_deallocatePositions.argtypes = [C.POINTER(Slices)]
+    for dims in ((8, 8, 8), (8, 8, 4), (4, 4, 4), (3, 5, 2)):
+        p = L.cubeUtils_diagonalSlices(*dims)
+        sp = p.contents
+        got = np.array([(sp.positions[i].x, sp.positions[i].y, sp.positions[i].z) for i in range(sp.length)])
+        assert np.array_equal(got, oracle.diagonal_slices(*dims)), dims
+        L.cubeUtils_deallocatePositions(p)
+
+
+def test_exp_golomb_host_matches_java_writer(pkg, oracle):
+    L = codec(pkg)
+    L.expGolomb_createStream.restype = C.POINTER(EGStream)
+    L.expGolomb_createStream.argtypes = [C.c_void_p]
+    L.expGolomb_writeValue.argtypes = [C.POINTER(EGStream), C.c_int]
+    L.expGolomb_readValue.argtypes = [C.POINTER(EGStream)]
+    rng = np.random.default_rng(5)
+    vals = np.concatenate([rng.integers(-700, 700, 5000), [0, 0, 0, 1, -1, 127, -128, 2**16, -2**16]])
+    buf = C.create_string_buffer(b"\xAA" * (vals.size * 8 + 16))  # dirty buffer: createStream zeroes
+    st = L.expGolomb_createStream(C.cast(buf, C.c_void_p))
+    for v in vals:
+        L.expGolomb_writeValue(st, int(v))
+    n = st.contents.bufferPosition
+    assert buf.raw[: n + 1] == oracle.eg_write(vals.astype(np.int32))
+    st2 = L.expGolomb_createStream(None)
+    st2.contents.buffer = C.cast(buf, C.c_void_p)
+    got = [L.expGolomb_readValue(st2) for _ in range(vals.size)]
+    assert np.array_equal(got, vals)
+
+
+def _ref_or_skip():
+    import oracle as o
+    if not os.path.exists(o.REF_LIB_PATH):
+        pytest.skip("oracle/_ref not built (reference sources absent)")
+    return C.CDLL(o.REF_LIB_PATH)
+
+
+def reference_entropy_encode(q, w, h, stacks, depth):
+    """encoder.c:143-296's entropy stage, driven with the reference's own functions."""
+    R = _ref_or_skip()
+    z = C.CDLL("libz.so.1")
+    z.zlibVersion.restype = C.c_char_p
+    R.cubeUtils_diagonalSlices.restype = C.c_void_p
+    R.expGolomb_createStream.restype = C.POINTER(EGStream)
+    R.expGolomb_createStream.argtypes = [C.c_void_p]
+    R.applyExpGolombCoding.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(EGStream)]
+    R.applyZlibCompression.argtypes = [C.POINTER(ZStream), C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+    R.expGolomb_freeBuffer.argtypes = [C.POINTER(EGStream), C.c_int, C.c_int]
+    buffer_size = w * h * depth
+    zs = ZStream()
+    assert z.deflateInit_(C.byref(zs), 9, z.zlibVersion(), C.sizeof(ZStream)) == 0  # Z_BEST_COMPRESSION
+    sp = R.cubeUtils_diagonalSlices(8, 8, depth)
+    egbuf = C.create_string_buffer(buffer_size * 4 + 16)  # zeroed (the reference mallocs: unzeroed byte 0)
+    st = R.expGolomb_createStream(C.cast(egbuf, C.c_void_p))
+    zout = C.create_string_buffer(buffer_size * 4 + 1024)
+    out = b""
+    per = buffer_size
+    for s in range(stacks):
+        f = np.ascontiguousarray(q[s * per:(s + 1) * per], np.float32)  # cl_float buffer of the stack
+        size = R.applyExpGolombCoding(f.ctypes.data, per, sp, st)
+        if s < stacks - 1:
+            n = R.applyZlibCompression(C.byref(zs), egbuf, size, zout, len(zout), 0)
+            R.expGolomb_freeBuffer(st, size, 1)
+        else:
+            n = R.applyZlibCompression(C.byref(zs), egbuf, size + 1, zout, len(zout), 1)
+        out += zout.raw[:n]
+    z.deflateEnd(C.byref(zs))
+    return out
+
+
+# depth 8 only: the reference C build hard-codes DCT_BLOCK_DEPTH 8 in codec.h:13 (an 8x8x4 reference
+# build would need an edited header); the 8x8x4 entropy stage is covered by the round-trip and
+# Java-payload tests below.
+@pytest.mark.parametrize("depth,kind,stacks", [(8, "ramp", 3), (8, "uniform", 2), (8, "ramp", 1)])
+def test_entropy_stage_bytes_match_reference_encoder(pkg, plan8, plan4, depth, kind, stacks):
+    w, h = 64, 48
+    plan = plan8 if depth == 8 else plan4
+    fr = pkg.synthetic.frames(w, h, depth * stacks, kind=kind)
+    q = plan.encode_q(fr).reshape(-1)
+    mine = entropy_encode(pkg, q, w, h, stacks, depth)
+    ref = reference_entropy_encode(q, w, h, stacks, depth)
+    assert mine == ref
+    # and the stream decodes back (host decoder) to the same coefficients
+    rc, back = entropy_decode(pkg, mine, w, h, stacks, depth)
+    assert rc == 0 and np.array_equal(back, q)
+
+
+def test_entropy_roundtrip_depth4(pkg, oracle, plan4):
+    fr = pkg.synthetic.frames(64, 48, 12, kind="uniform")
+    q = plan4.encode_q(fr).reshape(-1)
+    b = entropy_encode(pkg, q, 64, 48, 3, 4)
+    rc, back = entropy_decode(pkg, b, 64, 48, 3, 4)
+    assert rc == 0 and np.array_equal(back, q)
+    pos = oracle.diagonal_slices(8, 8, 4)
+    order = pos[:, 0] + pos[:, 1] * 8 + pos[:, 2] * 64
+    assert zlib.decompress(b) == oracle.eg_write(q.reshape(-1, 256)[:, order].reshape(-1))
+
+
+def test_entropy_payload_is_java_eg_of_diagonal_order(pkg, oracle, plan8):
+    """Inflated .bin payload == Java ExpGolombWriter over the diagonal order (Encoder.java:91-111):
+    the C container and the Java container carry the same payload (zlib row)."""
+    fr = pkg.synthetic.frames(64, 64, 8, kind="ramp")
+    q = plan8.encode_q(fr)
+    b = entropy_encode(pkg, q.reshape(-1), 64, 64, 1, 8)
+    payload = zlib.decompress(b)
+    pos = oracle.diagonal_slices()
+    order = pos[:, 0] + pos[:, 1] * 8 + pos[:, 2] * 64
+    java = oracle.eg_write(q.reshape(q.shape[0], -1)[:, order].reshape(-1))
+    assert payload == java
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_64x64x8.npz"))
+    assert payload == g["eg"].tobytes()
+
+
+def test_entropy_decoder_rejects_truncated(pkg, plan8):
+    fr = pkg.synthetic.frames(64, 64, 16, kind="uniform")
+    q = plan8.encode_q(fr).reshape(-1)
+    b = entropy_encode(pkg, q, 64, 64, 2, 8)
+    rc, _ = entropy_decode(pkg, b[: len(b) // 2], 64, 64, 2, 8)
+    assert rc != 0
+
+
+def test_read_cubes_quantisation_host_vs_reference(pkg, oracle, plan8, tmp_path):
+    R = _ref_or_skip()
+    L = codec(pkg)
+    libc = C.CDLL(None)
+    libc.fopen.restype = C.c_void_p
+    libc.fopen.argtypes = [C.c_char_p, C.c_char_p]
+    libc.fclose.argtypes = [C.c_void_p]
+    fr = pkg.synthetic.frames(64, 32, 8, kind="uniform")
+    p = tmp_path / "in.raw"
+    p.write_bytes(fr.tobytes())
+    outs = []
+    for lib in (R, L):
+        f = libc.fopen(str(p).encode(), b"rb")
+        d = np.zeros(fr.size, np.float32)
+        lib.readCubes.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        lib.readCubes(f, d.ctypes.data, 64, 32)
+        libc.fclose(f)
+        outs.append(d)
+    assert np.array_equal(outs[0], outs[1])
+    dct = oracle.to_cubes(plan8.dct(fr)).astype(np.float32).reshape(-1)
+    for name in ("applyQuantization", "applyDequantization"):
+        a, b = dct.copy(), dct.copy()
+        for lib, arr in ((R, a), (L, b)):
+            getattr(lib, name).argtypes = [C.c_void_p, C.c_size_t]
+            getattr(lib, name)(arr.ctypes.data, arr.size)
+        assert np.array_equal(a, b), name
+    # writeCubes: (unsigned char) truncation of the cube-major floats back to the raster
+    vals = (outs[0] * 0.999).astype(np.float32)
+    files = []
+    for i, lib in enumerate((R, L)):
+        path = tmp_path / f"out{i}.raw"
+        f = libc.fopen(str(path).encode(), b"wb")
+        lib.writeCubes.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        lib.writeCubes(f, vals.ctypes.data, 64, 32)
+        libc.fclose(f)
+        files.append(path.read_bytes())
+    assert files[0] == files[1]
