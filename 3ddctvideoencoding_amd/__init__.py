@@ -35,7 +35,7 @@ ABI_SYMBOLS = (
     "dct3d_reset_timers",
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
-    "dct3d_fill_synthetic_dev", "dct3d_plan_query",
+    "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev",
 )
 
 
@@ -95,6 +95,7 @@ def lib() -> C.CDLL:
         for name in ("dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev"):
             getattr(L, name).argtypes = [vp, vp, sz, vp]
         L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
+        L.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
         L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
         _lib = L
     return _lib
@@ -174,6 +175,8 @@ class Context:
 
     # ---- configuration ----
     def set_stream(self, hip_stream: Optional[int]) -> None:
+        """Run on an external hipStream_t.  None or 0 (e.g. torch's default stream, whose handle is 0)
+        selects the context's own stream -- use a non-default stream to share one with a framework."""
         _check(lib().dct3d_ctx_set_stream(self._h, hip_stream or None), "dct3d_ctx_set_stream")
 
     def set_profiling(self, on: bool) -> None:
@@ -244,6 +247,11 @@ class Context:
 
     def inverse_f32_dev(self, d_in, n_cubes: int, d_out) -> None:
         _check(lib().dct3d_inverse_f32_dev(self._h, _tptr(d_in), n_cubes, _tptr(d_out)), "dct3d_inverse_f32_dev")
+
+    def bandwidth_probe_dev(self, d_in, d_out, n_px: int, mode: int = 0) -> None:
+        _check(lib().dct3d_bandwidth_probe_dev(self._h, _tptr(d_in) if d_in is not None else None,
+                                               _tptr(d_out) if d_out is not None else None, n_px, mode),
+               "dct3d_bandwidth_probe_dev")
 
     def fill_synthetic_dev(self, d_frames, width: int, height: int, n_frames: int,
                            seed: int = synthetic.DEFAULT_SEED, frame0: int = 0, kind: str = "ramp") -> None:

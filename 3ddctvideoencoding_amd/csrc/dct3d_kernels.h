@@ -79,6 +79,7 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st);
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
+int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
 int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,
                  hipStream_t st);
 

@@ -58,6 +58,15 @@ __device__ __forceinline__ int java_round_dev(double a) {
 // butterflies of a pass (the compiler otherwise interleaves all of them and multiplies the live
 // temporaries, which costs occupancy).
 template <class T, int N>
+__device__ __forceinline__ void pin2(T (&x)[N], T (&y)[N]) {
+    static_assert(sizeof(T) == 4, "pin2: 32-bit values");
+    if constexpr (N == 8)
+        asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                          "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]), "+v"(y[6]), "+v"(y[7]));
+    else
+        asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]));
+}
+template <class T, int N>
 __device__ __forceinline__ void pin(T (&x)[N]) {
     if constexpr (sizeof(T) == 4) {
         if constexpr (N == 8)
@@ -78,7 +87,8 @@ __device__ __forceinline__ float byte_of(uint32_t w, int b) { return (float)((w 
 // Fused encode
 // =============================================================================================
 // Loads row y = j of frames 0..D-1 of cube g (row layout).
-template <int D>
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+template <int D, bool NTL = false>
 __device__ __forceinline__ void load_rows(const EncodeParams& P, uint32_t g, bool valid, int j, uint2 (&raw)[D]) {
     if (valid) {
         const uint32_t s = g / P.cubes_per_stack;
@@ -86,7 +96,14 @@ __device__ __forceinline__ void load_rows(const EncodeParams& P, uint32_t g, boo
         const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
         const uint8_t* src = P.raster + (size_t)s * P.stack_stride + (size_t)(by * 8 + j) * P.width + bx * 8;
 #pragma unroll
-        for (int z = 0; z < D; z++) raw[z] = *(const uint2*)(src + (size_t)z * P.plane);
+        for (int z = 0; z < D; z++) {
+            if constexpr (NTL) {
+                const u32x2_t t = __builtin_nontemporal_load((const u32x2_t*)(src + (size_t)z * P.plane));
+                raw[z] = make_uint2(t.x, t.y);
+            } else {
+                raw[z] = *(const uint2*)(src + (size_t)z * P.plane);
+            }
+        }
     } else {
 #pragma unroll
         for (int z = 0; z < D; z++) raw[z] = make_uint2(0u, 0u);
@@ -119,8 +136,8 @@ __device__ __forceinline__ void cube_stats(const uint2 (&raw)[D], const float (&
 #pragma unroll
         for (int x = 0; x < 8; x += 2) {
             const uint32_t u0 = __float_as_uint(a[z][x]), u1 = __float_as_uint(a[z][x + 1]);
-            mx = max(mx, max(u0, u1));
-            mn = min(mn, min(u0, u1));
+            asm("v_max3_u32 %0, %1, %2, %3" : "=v"(mx) : "v"(mx), "v"(u0), "v"(u1));
+            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mn) : "v"(mn), "v"(u0), "v"(u1));
         }
     }
 #pragma unroll
@@ -140,22 +157,29 @@ template <int D, int NB>
 __device__ __forceinline__ void forward_cube(float (&a)[D][8], int m, int c, int j, char* wl, float (&b)[8][NB]) {
     const float dcsub = 8.0f * (float)m;
     // pass X (integer front exact, cube-mean centring folded into X0), pass Z
+    pin(a[0]);
 #pragma unroll
     for (int z = 0; z < D; z++) {
-        pin(a[z]);
         fdct8<true, true>(a[z], dcsub);
-        pin(a[z]);
+        if (z + 1 < D) pin2(a[z], a[z + 1]);
+        else pin(a[z]);
     }
+    {
+        float col[8][D];
 #pragma unroll
-    for (int x = 0; x < 8; x++) {
-        float col[D];
+        for (int x = 0; x < 8; x++)
 #pragma unroll
-        for (int z = 0; z < D; z++) col[z] = a[z][x];
-        pin(col);
-        fdctN<D, false, false>(col, 0.f);
-        pin(col);
+            for (int z = 0; z < D; z++) col[x][z] = a[z][x];
 #pragma unroll
-        for (int z = 0; z < D; z++) a[z][x] = col[z];
+        for (int x = 0; x < 8; x++) {
+            fdctN<D, false, false>(col[x], 0.f);
+            if (x < 7) pin2(col[x], col[x + 1]);
+            else pin(col[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < 8; x++)
+#pragma unroll
+            for (int z = 0; z < D; z++) a[z][x] = col[x][z];
     }
     // LDS transpose: row layout (c, y)[kz][x] -> face layout (c, j)[y][kx']
     if constexpr (D == 8) {
@@ -189,16 +213,23 @@ __device__ __forceinline__ void forward_cube(float (&a)[D][8], int m, int c, int
         wave_lds_sync();
     }
     // pass Y
+    {
+        float col[NB][8];
 #pragma unroll
-    for (int x = 0; x < NB; x++) {
-        float col[8];
+        for (int x = 0; x < NB; x++)
 #pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = b[y][x];
-        pin(col);
-        fdct8<false, false>(col, 0.f);
-        pin(col);
+            for (int y = 0; y < 8; y++) col[x][y] = b[y][x];
+        pin(col[0]);
 #pragma unroll
-        for (int y = 0; y < 8; y++) b[y][x] = col[y];
+        for (int x = 0; x < NB; x++) {
+            fdct8<false, false>(col[x], 0.f);
+            if (x + 1 < NB) pin2(col[x], col[x + 1]);
+            else pin(col[x]);
+        }
+#pragma unroll
+        for (int x = 0; x < NB; x++)
+#pragma unroll
+            for (int y = 0; y < 8; y++) b[y][x] = col[x][y];
     }
 }
 
@@ -215,7 +246,7 @@ __device__ __forceinline__ void store16(void* p, const int4& v) {
 
 // One wave = ITER consecutive groups of 8 cubes; the rows of group it+1 are loaded (16 VGPRs)
 // before group it is transformed, so every wave keeps loads in flight while it computes.
-template <int D, int ITER, bool NT>
+template <int D, int ITER, bool NT, bool NTL = false>
 __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(EncodeParams P) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
@@ -232,7 +263,7 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
     const int so = kz + kx0;
 
     uint2 rawn[D];
-    load_rows<D>(P, group0 * kCubesPerWave + c, group0 * kCubesPerWave + c < P.n_cubes, j, rawn);
+    load_rows<D, NTL>(P, group0 * kCubesPerWave + c, group0 * kCubesPerWave + c < P.n_cubes, j, rawn);
 
 #pragma unroll 1
     for (int it = 0; it < ITER; it++) {
@@ -245,7 +276,7 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
         for (int z = 0; z < D; z++) raw[z] = rawn[z];
         if (it + 1 < ITER) {
             const uint32_t gn = cube0 + kCubesPerWave + c;
-            load_rows<D>(P, gn, gn < P.n_cubes, j, rawn);  // prefetch the next group
+            load_rows<D, NTL>(P, gn, gn < P.n_cubes, j, rawn);  // prefetch the next group
         }
 
         float a[D][8];
@@ -672,6 +703,76 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, int width, int
 }
 
 // =============================================================================================
+// Bandwidth calibration: the encode's traffic mix without the transform.  mode 0: read n_px bytes,
+// write 4*n_px (1:4, NT); mode 1: copy (NT); mode 2: write-only 4*n_px (NT); mode 3: read-only.
+// =============================================================================================
+__global__ __launch_bounds__(256) void ceiling_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                       long long n_px, int mode, unsigned* sink) {
+    // Pure streaming, every wave-instruction a contiguous 1 KiB: per iteration a thread reads 4
+    // 16-byte chunks (4 loads in flight) and writes 16 (mix 1:4), 4 (copy) or 16 (write-only).
+    const long long T = (long long)gridDim.x * blockDim.x;
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long n_in = n_px / 16;
+    unsigned acc = 0;
+    for (long long it = 0; it * 4 * T < n_in; it++) {
+        uint4 v[4];
+        if (mode != 2 && mode != 5) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const long long c = it * 4 * T + u * T + g;
+                if (c < n_in) {
+                    const i32x4_t t = __builtin_nontemporal_load((const i32x4_t*)(in + c * 16));
+                    v[u] = make_uint4((unsigned)t.x, (unsigned)t.y, (unsigned)t.z, (unsigned)t.w);
+                } else {
+                    v[u] = make_uint4(0, 0, 0, 0);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = make_uint4((unsigned)it, (unsigned)g, u, 0);
+        }
+        if (mode == 0 || mode == 2) {
+#pragma unroll
+            for (int w = 0; w < 16; w++) {
+                const long long o = it * 16 * T + w * T + g;
+                const uint4 x = v[w & 3];
+                if (o < 4 * n_in) store16<true>(out + o * 16, make_int4((int)x.x, (int)x.y, (int)x.z, (int)(x.w + w)));
+            }
+        } else if (mode == 1 || mode == 4) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const long long c = it * 4 * T + u * T + g;
+                const int4 o = make_int4((int)v[u].x, (int)v[u].y, (int)v[u].z, (int)v[u].w);
+                if (c < n_in) {
+                    if (mode == 1) store16<true>(out + c * 16, o);
+                    else *(int4*)(out + c * 16) = o;
+                }
+            }
+        } else if (mode == 5) {
+#pragma unroll
+            for (int w = 0; w < 16; w++) {
+                const long long o = it * 16 * T + w * T + g;
+                if (o < 4 * n_in) *(int4*)(out + o * 16) = make_int4((int)it, (int)g, w, 0);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st) {
+    static int grid = -1;
+    if (grid < 0) {
+        const char* e = getenv("DCT3D_PROBE_GRID");  // calibration knob: blocks of 256 threads
+        grid = e ? atoi(e) : 16384;  // best of the 1024..16384 sweep (profiles/r01/probe_sweep.txt)
+    }
+    hipLaunchKernelGGL(ceiling_kernel, dim3(grid), dim3(256), 0, st, in, out, n_px, mode, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// =============================================================================================
 // Launchers
 // =============================================================================================
 // Encode variants (template <D, ITER, NT>): ITER = 8-cube groups per wave (register prefetch
@@ -679,12 +780,12 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t* out, int width, int
 // DCT3D_ENC_VARIANT (test/bench knob) selects one; default kDefaultVariant.
 namespace {
 constexpr int kDefaultVariant = 1;
-template <int D, int ITER, bool NT>
+template <int D, int ITER, bool NT, bool NTL = false>
 void launch_enc_t(const EncodeParams& P, hipStream_t st) {
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t waves = (groups + ITER - 1) / ITER;
     const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode_kernel<D, ITER, NT>), dim3(blocks), dim3(kBlock), 0, st, P);
+    hipLaunchKernelGGL((encode_kernel<D, ITER, NT, NTL>), dim3(blocks), dim3(kBlock), 0, st, P);
 }
 template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
@@ -694,7 +795,8 @@ void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
         case 2: launch_enc_t<D, 4, false>(P, st); break;
         case 3: launch_enc_t<D, 4, true>(P, st); break;
         case 4: launch_enc_t<D, 16, false>(P, st); break;
-        default: launch_enc_t<D, 16, true>(P, st); break;
+        case 5: launch_enc_t<D, 16, true>(P, st); break;
+        default: launch_enc_t<D, 1, true, true>(P, st); break;  // 6: NT stores + NT loads
     }
 }
 }  // namespace

@@ -469,6 +469,13 @@ int dct3d_inverse_f32(dct3d_ctx* c, const float* in, size_t n_cubes, float* out)
     return cube_f32_host(c, in, n_cubes, out, true);
 }
 
+int dct3d_bandwidth_probe_dev(dct3d_ctx* c, const uint8_t* d_in, void* d_out, size_t n_px, int mode) {
+    if (!c || n_px % 16 || mode < 0 || mode > 5 || (mode != 2 && mode != 5 && !d_in) || (mode != 3 && !d_out)) return DCT3D_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    return launch_ceiling(d_in, (uint8_t*)d_out, (long long)n_px, mode, (unsigned*)c->d_counters.p, c->stream)
+               ? DCT3D_EKERNEL : DCT3D_OK;
+}
+
 int dct3d_fill_synthetic_dev(dct3d_ctx* c, uint8_t* d, int w, int h, int n_frames, uint64_t seed, int64_t frame0,
                              int kind) {
     if (!c || !d || w <= 0 || h <= 0 || n_frames < 0 || (kind != 0 && kind != 1)) return DCT3D_EINVAL;

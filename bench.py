@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--kind", default="ramp", choices=["ramp", "uniform"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true")
     return ap.parse_args()
 
 
@@ -73,6 +74,26 @@ def cpu_baseline(width, height, depth, budget_s, kind):
                       f"DCT.run + Encoder quantisation, {threads} threads, {t_total:.1f} s"}
 
 
+def measure_ceiling(ctx, torch, frames, q, reps):
+    """Achievable HBM rates on this device for the path's traffic mix, same buffers, same stream:
+    mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only."""
+    n_px = frames.numel() // 16 * 16
+    out = {}
+    for name, mode, bytes_per_px in (("mix_1r4w", 0, 5), ("copy", 1, 2), ("write", 2, 4), ("write_plain", 5, 4),
+                                      ("read", 3, 1)):
+        ctx.bandwidth_probe_dev(frames, q, n_px, mode)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            ctx.bandwidth_probe_dev(frames, q, n_px, mode)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        out[name + "_GBs"] = n_px * bytes_per_px / (ms * 1e-3) / 1e9
+    return out
+
+
 def main():
     a = parse()
     width, height, depth, stacks, direction = CONFIGS[a.config]
@@ -97,7 +118,10 @@ def main():
 
     pkg = importlib.import_module("3ddctvideoencoding_amd")
     ctx = pkg.Context(dev, 8, 8, depth)
-    stream = torch.cuda.current_stream()
+    # a dedicated stream: the library, torch's events and torch's allocations all use it (torch's
+    # default stream has handle 0, which the C-ABI reads as "use the context's own stream")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     n_cubes = ctx.n_cubes(width, height, stacks)
@@ -134,6 +158,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
     ctx.set_profiling(False)
+    ceiling = None if a.no_ceiling else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
     sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
     elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
 
@@ -179,6 +204,7 @@ def main():
             "fixup_ms": fixup_ms,
             "bytes_per_cube": bytes_per_cube,
         },
+        "ceiling": ceiling,
         "flagged_units_last_step": st["n_flagged"],
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,

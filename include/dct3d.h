@@ -158,6 +158,12 @@ int dct3d_inverse_f32_dev(dct3d_ctx *ctx, const float *d_coeffs, size_t n_cubes,
 int dct3d_fill_synthetic_dev(dct3d_ctx *ctx, uint8_t *d_frames, int width, int height, int n_frames,
                              uint64_t seed, int64_t frame0, int kind);
 
+/* Bandwidth calibration (bench support): the encode's traffic pattern without the transform, on the
+ * context stream.  mode 0: d_in u8 [n_px] -> d_out int32 [n_px] (1 B read : 4 B written, NT stores);
+ * mode 1: copy n_px bytes; mode 2: write 4*n_px bytes; mode 3: read n_px bytes; modes 4/5: copy /
+ * write with plain (temporal) stores.  n_px % 16 == 0. */
+int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, size_t n_px, int mode);
+
 #ifdef __cplusplus
 }
 #endif
