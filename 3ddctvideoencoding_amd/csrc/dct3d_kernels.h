@@ -63,7 +63,7 @@ struct DecodeFixupParams {
     const unsigned int* counters;
     uint32_t flag_cap;
     const uint32_t* cube_list;
-    const double* inv_coef;    // [cs * cs]
+    const double* inv_coef_t;  // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
 };
 
 struct Fwd64Params {

@@ -33,6 +33,7 @@ CONFIGS = {
     "c3_decode_1080p": (1920, 1080, 8, 128, "decode"),
     "c4_encode_4k": (3840, 2160, 8, 8, "encode"),
     "c5_encode_1080p_d4": (1920, 1080, 4, 128, "encode"),
+    "c6_decode_1080p_d4": (1920, 1080, 4, 128, "decode"),
 }
 
 

@@ -7,7 +7,7 @@
 # Each pass under its own timeout; stops at the first crash/timeout.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=gpurun_out/prof${PROF_TAG:+_$PROF_TAG}
 mkdir -p $OUT
 ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3 --no-cpu-baseline"}
 run() {
@@ -18,6 +18,7 @@ run() {
   case $rc in 0) ;; *) exit $rc;; esac
 }
 run trace --kernel-trace --stats
+[ -n "$TRACE_ONLY" ] && exit 0
 run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 find $OUT -name "*.csv" | head -20
