@@ -681,83 +681,114 @@ __device__ __forceinline__ uint32_t cvt_u32_sat(double v) {
     return t;
 }
 
+// staged input of one tile (CPW cubes, 8 KiB): 8 coalesced 1 KiB loads per wave
 template <int D>
-__global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
+__device__ __forceinline__ void dec_load_tile(const DecodeParams& P, uint32_t cube0, int lane, int4 (&v)[8]) {
     using G = DecGeom<D>;
-    constexpr int CS = G::CS, CPW = G::CPW;
-    constexpr int NXC = (D == 8) ? 4 : 8;  // x values per lane in layout C
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    char* wl = lds + wave * kDecWaveLds;
-    const int h = (lane >> 4) & 1;
-    const int k = lane & (D - 1);
-    const int c = (lane >> 5) * (CPW / 2) + ((lane & 15) / D);
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * CPW;
-    const uint32_t g = cube0 + c;
-    const bool valid = g < P.n_cubes;
-
-    // ---- staged loads: 8 x 1 KiB per wave -> padded faces ----
-    {
-        const char* inb = (const char*)(P.in + (size_t)cube0 * CS);
-        int4 v[8];
-        if (cube0 + CPW <= P.n_cubes) {  // wave-uniform: every cube of the wave exists
+    const char* inb = (const char*)(P.in + (size_t)cube0 * G::CS);
+    if (cube0 + G::CPW <= P.n_cubes) {  // wave-uniform: every cube of the tile exists
 #pragma unroll
-            for (int t = 0; t < 8; t++) v[t] = *(const int4*)(inb + (size_t)(t * 64 + lane) * 16);
-        } else {
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-                const int q = t * 64 + lane;
-                v[t] = make_int4(0, 0, 0, 0);
-                if (cube0 + q / (CS / 4) < P.n_cubes) v[t] = *(const int4*)(inb + (size_t)q * 16);
-            }
-        }
+        for (int t = 0; t < 8; t++) v[t] = *(const int4*)(inb + (size_t)(t * 64 + lane) * 16);
+    } else {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
             const int q = t * 64 + lane;
-            *(int4*)(wl + (q / (CS / 4)) * G::SA_C + ((q >> 4) % D) * G::SA_F + (q & 15) * 16) = v[t];
+            v[t] = make_int4(0, 0, 0, 0);
+            if (cube0 + q / (G::CS / 4) < P.n_cubes) v[t] = *(const int4*)(inb + (size_t)q * 16);
         }
     }
-    wave_lds_sync();
+}
+template <int D>
+__device__ __forceinline__ void dec_stage_tile(char* wl, int lane, const int4 (&v)[8]) {
+    using G = DecGeom<D>;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int q = t * 64 + lane;
+        *(int4*)(wl + (q / (G::CS / 4)) * G::SA_C + ((q >> 4) % D) * G::SA_F + (q & 15) * 16) = v[t];
+    }
+}
 
-    // ---- layout A: dequantise (exact integers in fp64), amax ----
+// One tile (CPW cubes) from the staged input in the wave's LDS region to the raster.  after_a() runs
+// once the staged input is in registers (the persistent variant issues the next tile's loads there).
+// PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
+template <int D, int PG, class AfterA>
+__device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
+                                            AfterA&& after_a) {
+    using G = DecGeom<D>;
+    constexpr int CS = G::CS, CPW = G::CPW;
+    constexpr int NXC = (D == 8) ? 4 : 8;  // x values per lane in layout C
+    const int h = (lane >> 4) & 1;
+    const int k = lane & (D - 1);
+    const int c = (lane >> 5) * (CPW / 2) + ((lane & 15) / D);
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+
+    // ---- layout A: dequantise, amax ----
+    // cf = q * step exactly: a 24-bit integer multiply (|q| < 2^23 checked; |q * step| < 2^30), then
+    // an exact conversion to fp64.  Out-of-range q (never produced by the encoder) sends the cube to
+    // the exact replay.  amax = max |q * step| from integer max / min.
     double b[8][4];
-    double amax = 0.0;
+    float amax_f;
+    bool q_range_bad;
     {
-        const double s_base = 5.0 * (double)(4 * h + k);      // step = s_base + 5 (e + ky), DC: 1
-        const double s_dc = fmax(s_base, 1.0);
+        const int sb = 5 * (4 * h + k);                     // step = sb + 5 (e + ky); DC (e = ky = 0): 1
+        int stp[11];
+        stp[0] = max(sb, 1);
+#pragma unroll
+        for (int j = 1; j < 11; j++) stp[j] = sb + 5 * j;
         const char* src = wl + c * G::SA_C + k * G::SA_F + h * 16;
+        int4 raw[8];  // all eight LDS reads in flight before the first use
+#pragma unroll
+        for (int ky = 0; ky < 8; ky++) raw[ky] = *(const int4*)(src + ky * 32);
+        int qmax = INT32_MIN, qmin = INT32_MAX, tmax = 0, tmin = 0;
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) {
-            const int4 v = *(const int4*)(src + ky * 32);
-            const int vv[4] = {v.x, v.y, v.z, v.w};
+            const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
+            int t[4];
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                const double qd = (double)vv[e];
-                double cf;
-                if (ky == 0 && e == 0) cf = qd * s_dc;
-                else cf = __builtin_fma(qd, (double)(5 * (e + ky)), qd * s_base);  // exact
-                b[ky][e] = cf;
-                amax = fmax(amax, fabs(cf));
+                t[e] = __mul24(vv[e], stp[e + ky]);
+                b[ky][e] = (double)t[e];
             }
-            pin(b[ky]);
+            qmax = max(qmax, max(max(vv[0], vv[1]), max(vv[2], vv[3])));
+            qmin = min(qmin, min(min(vv[0], vv[1]), min(vv[2], vv[3])));
+            tmax = max(tmax, max(max(t[0], t[1]), max(t[2], t[3])));
+            tmin = min(tmin, min(min(t[0], t[1]), min(t[2], t[3])));
         }
+        q_range_bad = (qmax > 0x7FFFFF) | (qmin < -0x800000);
+        // float upper bound of amax (nearest rounding is within 2^-24 relative; the product with
+        // 1 + 2^-22 rounds to at least amax): the cube reduction then moves one dword per step
+        amax_f = (float)max(tmax, -tmin) * (1.0f + 0x1p-22f);
     }
-    // amax over the cube's lanes: xor over the k bits and bit 4
-#pragma unroll
-    for (int o = 1; o < D; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o, 64));
-    amax = fmax(amax, __shfl_xor(amax, 16, 64));
+    after_a();
+    // amax over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
+    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0xB1, 0xF, 0xF, false)));  // quad_perm xor 1
+    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x4E, 0xF, 0xF, false)));  // quad_perm xor 2
+    if constexpr (D == 8)
+        amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+    {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, amax_f), __builtin_bit_cast(uint32_t, amax_f), false, false);
+        amax_f = fmaxf(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+    }
+    const double amax = (double)amax_f;
 
     // ---- inverse pass Y ----
+    constexpr int G1 = PG == 0 ? 4 : PG;
 #pragma unroll
-    for (int e = 0; e < 4; e++) {
-        double col[8];
+    for (int e0 = 0; e0 < 4; e0 += G1) {
+        double col[G1][8];
 #pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = b[y][e];
-        pin(col);
-        idct8(col);
-        pin(col);
+        for (int i = 0; i < G1; i++)
 #pragma unroll
-        for (int y = 0; y < 8; y++) b[y][e] = col[y];
+            for (int y = 0; y < 8; y++) col[i][y] = b[y][e0 + i];
+        if (PG) for (int i = 0; i < G1; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++) idct8(col[i]);
+        if (PG) for (int i = 0; i < G1; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int y = 0; y < 8; y++) b[y][e0 + i] = col[i][y];
     }
 
     // ---- A -> B: swap the off-diagonal 4x4 blocks of the lane pair (l, l^16) ----
@@ -769,21 +800,26 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
 
     // ---- inverse pass X ----
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-        double row[8];
+    for (int r0 = 0; r0 < 4; r0 += G1) {
+        double row[G1][8];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            row[e] = b[r][e];
-            row[4 + e] = b[4 + r][e];
-        }
-        pin(row);
-        idct8(row);
-        pin(row);
+        for (int i = 0; i < G1; i++)
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            b[r][e] = row[e];
-            b[4 + r][e] = row[4 + e];
-        }
+            for (int e = 0; e < 4; e++) {
+                row[i][e] = b[r0 + i][e];
+                row[i][4 + e] = b[4 + r0 + i][e];
+            }
+        if (PG) for (int i = 0; i < G1; i++) pin(row[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++) idct8(row[i]);
+        if (PG) for (int i = 0; i < G1; i++) pin(row[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                b[r0 + i][e] = row[i][e];
+                b[4 + r0 + i][e] = row[i][4 + e];
+            }
     }
 
     // ---- B -> C through LDS in two rounds (D=8: z halves, D=4: x halves); every lane reads in
@@ -832,24 +868,31 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     }
 
     // ---- inverse pass Z ----
+    constexpr int G3 = PG == 0 ? NXC : PG;
 #pragma unroll
-    for (int e = 0; e < NXC; e++) {
-        double col[D];
+    for (int e0 = 0; e0 < NXC; e0 += G3) {
+        double col[G3][D];
 #pragma unroll
-        for (int z = 0; z < D; z++) col[z] = cz[z][e];
-        pin(col);
-        idctN<D>(col);
-        pin(col);
+        for (int i = 0; i < G3; i++)
 #pragma unroll
-        for (int z = 0; z < D; z++) cz[z][e] = col[z];
+            for (int z = 0; z < D; z++) col[i][z] = cz[z][e0 + i];
+        if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G3; i++) idctN<D>(col[i]);
+        if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G3; i++)
+#pragma unroll
+            for (int z = 0; z < D; z++) cz[z][e0 + i] = col[i][z];
     }
 
     // ---- certify, clamp + truncate, store ----
     const double m = amax * P.dec_G + P.dec_E + 0x1p-43;
     const int y = (D == 8) ? k : (4 * h + k);
     const int x0 = (D == 8) ? 4 * h : 0;
-    bool flag = false;
+    bool flag = q_range_bad;
     uint32_t outw[D][NXC / 4];
+    const uint32_t c255 = 255u;
 #pragma unroll
     for (int z = 0; z < D; z++) {
 #pragma unroll
@@ -860,7 +903,11 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
                 const double v = cz[z][4 * wd + e];
                 const uint32_t tl = cvt_u32_sat(v - m), th = cvt_u32_sat(v + m);
                 flag |= tl != th;
-                w |= min(tl, 255u) << (8 * e);
+                // byte e of w = min(tl, 255) (SDWA byte insert: the other bytes are preserved)
+                if (e == 0) w = min(tl, 255u);
+                else if (e == 1) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
+                else if (e == 2) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
+                else asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
             }
             asm volatile("" : "+v"(w));  // one output word at a time (bounded live range)
             outw[z][wd] = w;
@@ -889,6 +936,60 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
             P.cube_list[idx] = g;
         }
     }
+}
+
+template <int D, int PG>
+__global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    char* wl = lds + wave * kDecWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * DecGeom<D>::CPW;
+    int4 v[8];
+    dec_load_tile<D>(P, cube0, lane, v);
+    dec_stage_tile<D>(wl, lane, v);
+    wave_lds_sync();
+    decode_tile<D, PG>(P, wl, lane, cube0, [] {});
+}
+
+// DIAGNOSTIC variants (DCT3D_DEC_VARIANT=7 / 8; the output is NOT a decode): MODE 1 = memory only
+// (the same loads, staging and raster stores, no transform), MODE 2 = compute only (no global loads;
+// stores suppressed by a runtime condition).  They split the kernel's time into its memory and compute
+// parts (1.9 ms / 1.8 ms against 2.25 ms for the full kernel, c3).
+template <int D, int MODE>
+__global__ __launch_bounds__(kBlock, 4) void decode_kernel_diag(DecodeParams P) {
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
+    using G = DecGeom<D>;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    char* wl = lds + wave * kDecWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * G::CPW;
+    int4 v[8];
+    if (MODE == 2) {
+        for (int t = 0; t < 8; t++) v[t] = make_int4(lane + t, (int)cube0 & 7, t, 1);
+    } else {
+        dec_load_tile<D>(P, cube0, lane, v);
+    }
+    dec_stage_tile<D>(wl, lane, v);
+    wave_lds_sync();
+    if (MODE == 1) {
+        const int h = (lane >> 4) & 1, k = lane & (D - 1);
+        const int c = (lane >> 5) * (G::CPW / 2) + ((lane & 15) / D);
+        const uint32_t g = cube0 + c;
+        uint32_t acc = 0;
+        for (int ky = 0; ky < 8; ky++) {
+            const int4 x = *(const int4*)(wl + c * G::SA_C + k * G::SA_F + h * 16 + ky * 32);
+            acc += x.x ^ x.y ^ x.z ^ x.w;
+        }
+        if (g < P.n_cubes) {
+            const uint32_t s = g / P.cubes_per_stack, rr = g - s * P.cubes_per_stack;
+            const uint32_t by = rr / P.nbx, bx = rr - by * P.nbx;
+            uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + k) * P.width + bx * 8 + 4 * h;
+            for (int z = 0; z < D; z++) *(uint32_t*)(dst + (size_t)z * P.plane) = acc + z;
+        }
+        return;
+    }
+    DecodeParams Q = P;
+    if (MODE == 2 && P.width != 0xFFFFFFFFu) Q.n_cubes = 0;  // all stores suppressed, compute kept
+    decode_tile<D, 1>(Q, wl, lane, cube0, [] {});
 }
 
 // Exact Java InverseDCT fold (InverseDCT.java:56-66: k ascending, zero coefficients skipped, then
@@ -1110,6 +1211,12 @@ int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template <int PG>
+static void launch_dec_t(int D, uint32_t groups, const DecodeParams& P, hipStream_t st) {
+    if (D == 8) hipLaunchKernelGGL((decode_kernel<8, PG>), dim3(groups), dim3(kBlock), 0, st, P);
+    else hipLaunchKernelGGL((decode_kernel<4, PG>), dim3(groups), dim3(kBlock), 0, st, P);
+}
+
 int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     static int variant = -1;
@@ -1126,8 +1233,15 @@ int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
         const uint32_t per = (D == 8 ? DecGeom<8>::CPW : DecGeom<4>::CPW) * kWavesPerBlock;
         const uint32_t groups = (uint32_t)((P.n_cubes + per - 1) / per);
         // (non-temporal dword output stores were measured 26 % slower: 3.18 vs 2.51 ms, c3)
-        if (D == 8) hipLaunchKernelGGL(decode_kernel<8>, dim3(groups), dim3(kBlock), 0, st, P);
-        else hipLaunchKernelGGL(decode_kernel<4>, dim3(groups), dim3(kBlock), 0, st, P);
+        // 1: one butterfly per pin group (default); 4: unpinned (pin groups 1/2/4/none measured
+        // within 1 %); 7 / 8: diagnostics, memory-only / compute-only (output NOT valid)
+        switch (variant) {
+            case 4: launch_dec_t<0>(D, groups, P, st); break;
+            case 7: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, st, P); break;
+            case 8: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, st, P); break;
+
+            default: launch_dec_t<1>(D, groups, P, st); break;
+        }
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
