@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "dct3d_codec")
 REPO_DIR = os.path.dirname(PKG_DIR)
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
-DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL = 0, 1, 2, 3, 4
+DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC = 0, 1, 2, 3, 4, 5
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -97,6 +97,10 @@ def lib() -> C.CDLL:
         L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
         L.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
         L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
+        L.dct3d_eg_encode_dev.argtypes = [vp, vp, u64, C.c_uint8, i32, vp, u64, C.POINTER(u64)]
+        L.dct3d_encode_eg.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, C.POINTER(u64)]
+        L.dct3d_eg_fetch.argtypes = [vp, vp, u64]
+        L.dct3d_diagonal_order.argtypes = [i32, i32, i32, vp]
         _lib = L
     return _lib
 
@@ -143,6 +147,19 @@ def plan_query(block_w: int = 8, block_h: int = 8, block_d: int = 8) -> dict:
             "enc_rstep": np.array(info.enc_rstep[:]), "enc_G": np.array(info.enc_G[:]),
             "enc_E": np.array(info.enc_E[:]), "ngroups": ng, "coef": coef.reshape(cs, 64),
             "group_of": gof.reshape(cs, cs), "enc_K": K}
+
+
+def diagonal_order(block_w: int = 8, block_h: int = 8, block_d: int = 8) -> np.ndarray:
+    """Diagonal-slice order used by the device Exp-Golomb stage: cube index x + 8y + 64z per stream
+    position (CubeUtils.c:5-46)."""
+    out = np.empty(block_w * block_h * block_d, np.uint16)
+    _check(lib().dct3d_diagonal_order(block_w, block_h, block_d, _ptr(out)), "dct3d_diagonal_order")
+    return out
+
+
+def eg_stream_bytes(total_bits: int) -> int:
+    """Bytes holding a stream of total_bits bits (the last one partial)."""
+    return (total_bits + 7) // 8
 
 
 class Context:
@@ -252,6 +269,29 @@ class Context:
         _check(lib().dct3d_bandwidth_probe_dev(self._h, _tptr(d_in) if d_in is not None else None,
                                                _tptr(d_out) if d_out is not None else None, n_px, mode),
                "dct3d_bandwidth_probe_dev")
+
+    # ---- Exp-Golomb stage ----
+    def eg_encode_dev(self, d_q, n_cubes: int, d_out, out_cap: int, carry_byte: int = 0, carry_bits: int = 0) -> int:
+        """Device Exp-Golomb stream of n_cubes int32 cubes into d_out (4-byte aligned words); returns the
+        total bits (carry included).  Raises Dct3dError(DCT3D_ENOSPC) when out_cap is too small."""
+        tb = C.c_uint64(0)
+        _check(lib().dct3d_eg_encode_dev(self._h, _tptr(d_q), n_cubes, carry_byte, carry_bits, _tptr(d_out), out_cap,
+                                         C.byref(tb)), "dct3d_eg_encode_dev")
+        return tb.value
+
+    def encode_eg(self, frames: np.ndarray, carry_byte: int = 0, carry_bits: int = 0) -> tuple[bytes, int]:
+        """u8 frames [n_stacks*bd, H, W] -> (Exp-Golomb stream bytes, total bits), computed on the device
+        (DCT + quantisation + diagonal order + Exp-Golomb); only the stream crosses PCIe."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        F, H, W = frames.shape
+        if F % self.bd:
+            raise ValueError("frame count must be a multiple of the block depth")
+        tb = C.c_uint64(0)
+        _check(lib().dct3d_encode_eg(self._h, _ptr(frames), W, H, F // self.bd, carry_byte, carry_bits, C.byref(tb)),
+               "dct3d_encode_eg")
+        out = np.empty(eg_stream_bytes(tb.value), np.uint8)
+        _check(lib().dct3d_eg_fetch(self._h, _ptr(out) if out.size else None, out.size), "dct3d_eg_fetch")
+        return out.tobytes(), tb.value
 
     def fill_synthetic_dev(self, d_frames, width: int, height: int, n_frames: int,
                            seed: int = synthetic.DEFAULT_SEED, frame0: int = 0, kind: str = "ramp") -> None:

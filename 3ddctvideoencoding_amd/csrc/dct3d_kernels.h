@@ -77,7 +77,21 @@ int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
 int launch_encode(int D, const EncodeParams& P, hipStream_t st);
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
+struct EgParams {
+    const int32_t* q;          // cube-major quantised values
+    uint64_t n_cubes;
+    const uint16_t* diag;      // [cs] diagonal-slice order: cube index x + 8y + 64z per stream position
+    uint32_t* bits;            // [n_cubes] bits per cube
+    uint64_t* off;             // [n_cubes] stream bit offset of each cube (carry included)
+    uint64_t* bsum;            // [n_chunks] chunk sums -> chunk offsets
+    uint64_t* status;          // [0] total bits (carry included), [1] flags: 1 capacity, 2 value range
+    uint32_t* out;             // output words (memory byte order), capacity out_cap_words
+    uint64_t out_cap_words;
+    uint32_t carry_bits, carry_byte;
+};
+
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
+int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
 int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
 int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,

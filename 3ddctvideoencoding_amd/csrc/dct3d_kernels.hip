@@ -715,7 +715,7 @@ template <int D, int PG, class AfterA>
 __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
                                             AfterA&& after_a) {
     using G = DecGeom<D>;
-    constexpr int CS = G::CS, CPW = G::CPW;
+    constexpr int CPW = G::CPW;
     constexpr int NXC = (D == 8) ? 4 : 8;  // x values per lane in layout C
     const int h = (lane >> 4) & 1;
     const int k = lane & (D - 1);

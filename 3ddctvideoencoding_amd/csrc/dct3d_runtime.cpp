@@ -66,7 +66,23 @@ struct dct3d_ctx {
     bool last_valid = false;
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
+    // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
+    DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q;
+    uint64_t eg_last_bytes = 0;
 };
+
+// diagonal-slice order (CubeUtils.c:5-46): x + y + z ascending; y outer, z middle, x inner
+static int diagonal_order(int bw, int bh, int bd, uint16_t* out) {
+    int n = 0;
+    for (int t = 0; t <= (bw - 1) + (bh - 1) + (bd - 1); t++)
+        for (int y = 0; y <= (bh - 1 < t ? bh - 1 : t); y++)
+            for (int z = 0; z <= (bd - 1 < t ? bd - 1 : t); z++) {
+                const int x = t - y - z;
+                if (x < 0 || x > bw - 1) continue;
+                out[n++] = (uint16_t)(x + bw * y + bw * bh * z);
+            }
+    return n;
+}
 
 extern "C" {
 
@@ -79,6 +95,7 @@ const char* dct3d_strerror(int code) {
         case DCT3D_EDEVICE: return "HIP device error";
         case DCT3D_ENOMEM: return "out of memory";
         case DCT3D_EKERNEL: return "kernel launch failed";
+        case DCT3D_ENOSPC: return "output buffer too small";
         default: return "unknown error";
     }
 }
@@ -154,6 +171,12 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
     }
     if (!rc) rc = upload(c->d_tabs, tabs, sizeof(tabs));
     if (!rc) rc = c->d_counters.grow(16);
+    if (!rc) {
+        std::vector<uint16_t> diag(p.cs);
+        diagonal_order(block_w, block_h, block_d, diag.data());
+        rc = upload(c->d_diag, diag.data(), diag.size() * sizeof(uint16_t));
+    }
+    if (!rc) rc = c->d_eg_status.grow(16);
     if (rc) {
         dct3d_ctx_destroy(c);
         return rc;
@@ -167,7 +190,8 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
-                      &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux})
+                      &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
+                      &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -491,6 +515,101 @@ int dct3d_fill_synthetic_dev(dct3d_ctx* c, uint8_t* d, int w, int h, int n_frame
     if (!c || !d || w <= 0 || h <= 0 || n_frames < 0 || (kind != 0 && kind != 1)) return DCT3D_EINVAL;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     return launch_synth(d, w, h, (long long)w * h * n_frames, seed, frame0, kind, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
+}
+
+// ---- Exp-Golomb stage ----------------------------------------------------------------------------
+int dct3d_diagonal_order(int bw, int bh, int bd, uint16_t* out) {
+    if (!out || bw != 8 || bh != 8 || (bd != 8 && bd != 4)) return DCT3D_EINVAL;
+    diagonal_order(bw, bh, bd, out);
+    return DCT3D_OK;
+}
+
+static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t carry_byte, int carry_bits,
+                  uint32_t* d_out, uint64_t out_cap, uint64_t* total_bits) {
+    const uint64_t n_chunks = (n_cubes + 4095) / 4096;
+    int rc = c->d_eg_bits.grow(n_cubes * sizeof(uint32_t));
+    if (!rc) rc = c->d_eg_off.grow(n_cubes * sizeof(uint64_t));
+    if (!rc) rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t));
+    if (rc) return rc;
+    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    EgParams P;
+    P.q = d_q;
+    P.n_cubes = n_cubes;
+    P.diag = (const uint16_t*)c->d_diag.p;
+    P.bits = (uint32_t*)c->d_eg_bits.p;
+    P.off = (uint64_t*)c->d_eg_off.p;
+    P.bsum = (uint64_t*)c->d_eg_bsum.p;
+    P.status = (uint64_t*)c->d_eg_status.p;
+    P.out = d_out;
+    P.out_cap_words = out_cap / 4;
+    P.carry_bits = (uint32_t)carry_bits;
+    P.carry_byte = carry_byte;
+    if (launch_eg_encode(c->bd, P, c->stream)) return DCT3D_EKERNEL;
+    uint64_t st[2] = {0, 0};
+    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    if (total_bits) *total_bits = st[0];
+    if (st[1] & 2) return DCT3D_EINVAL;
+    if (st[1] & 1) return DCT3D_ENOSPC;
+    return DCT3D_OK;
+}
+
+int dct3d_eg_encode_dev(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t carry_byte, int carry_bits,
+                        uint8_t* d_out, uint64_t out_cap, uint64_t* total_bits) {
+    if (!c || carry_bits < 0 || carry_bits > 7 || (n_cubes && (!d_q || !d_out)) || ((uintptr_t)d_out & 3))
+        return DCT3D_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    if (n_cubes == 0) {
+        if (total_bits) *total_bits = (uint64_t)carry_bits;
+        if (carry_bits == 0) return DCT3D_OK;
+        if (out_cap < 4) return DCT3D_ENOSPC;
+        const uint32_t w = carry_byte & (0xFF00u >> carry_bits);
+        return hipMemcpy(d_out, &w, 4, hipMemcpyHostToDevice) == hipSuccess ? DCT3D_OK : DCT3D_EDEVICE;
+    }
+    return eg_run(c, d_q, n_cubes, carry_byte, carry_bits, (uint32_t*)d_out, out_cap, total_bits);
+}
+
+int dct3d_encode_eg(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n_stacks, uint8_t carry_byte,
+                    int carry_bits, uint64_t* total_bits) {
+    if (!c || (!raster && n_stacks) || carry_bits < 0 || carry_bits > 7) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    c->eg_last_bytes = 0;
+    const size_t in_bytes = n_cubes * c->plan.cs;
+    if ((rc = c->h_in.grow(in_bytes ? in_bytes : 1)) || (rc = c->d_eg_q.grow((in_bytes ? in_bytes : 1) * sizeof(int32_t))))
+        return rc;
+    if (n_cubes && hipMemcpyAsync(c->h_in.p, raster, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    if (n_cubes && (rc = dct3d_encode_stacks_dev(c, (const uint8_t*)c->h_in.p, w, h, n_stacks, (int32_t*)c->d_eg_q.p, nullptr)))
+        return rc;
+    // first try: 1 byte per value (8 bits / value; typical content needs 1.5-4), grown to fit on ENOSPC
+    uint64_t cap = in_bytes + 64, tb = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if ((rc = c->d_eg_out.grow(cap))) return rc;
+        rc = n_cubes ? eg_run(c, (const int32_t*)c->d_eg_q.p, n_cubes, carry_byte, carry_bits, (uint32_t*)c->d_eg_out.p,
+                              c->d_eg_out.bytes, &tb)
+                     : dct3d_eg_encode_dev(c, nullptr, 0, carry_byte, carry_bits, (uint8_t*)c->d_eg_out.p,
+                                           c->d_eg_out.bytes, &tb);
+        if (rc != DCT3D_ENOSPC) break;
+        cap = (tb + 31) / 32 * 4 + 64;
+    }
+    if (rc) return rc;
+    if (total_bits) *total_bits = tb;
+    c->eg_last_bytes = (tb + 7) / 8;
+    return DCT3D_OK;
+}
+
+int dct3d_eg_fetch(dct3d_ctx* c, uint8_t* out, uint64_t nbytes) {
+    if (!c || (nbytes && !out) || nbytes > c->eg_last_bytes) return DCT3D_EINVAL;
+    if (nbytes == 0) return DCT3D_OK;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    if (hipMemcpyAsync(out, c->d_eg_out.p, nbytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    return DCT3D_OK;
 }
 
 }  // extern "C"

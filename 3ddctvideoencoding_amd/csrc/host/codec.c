@@ -53,11 +53,17 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
     }
     const size_t frame = (size_t)width * height, stack_px = frame * depth;
     const int n_stacks = (frames + depth - 1) / depth;
+    /* DCT3D_CODEC_HOST_EG=1: Exp-Golomb on the host from the quantised ints (A/B and tests); default:
+     * the device Exp-Golomb stage, the same bytes */
+    const char *he = getenv("DCT3D_CODEC_HOST_EG");
+    const int host_eg = he && he[0] == '1';
     uint8_t *raster = (uint8_t *)malloc(stack_px * batch);
-    int32_t *q = (int32_t *)malloc(stack_px * batch * sizeof(int32_t));
+    int32_t *q = host_eg ? (int32_t *)malloc(stack_px * batch * sizeof(int32_t)) : NULL;
+    size_t eg_cap = stack_px * batch / 2 + 64;
+    unsigned char *eg = host_eg ? NULL : (unsigned char *)malloc(eg_cap);
     dct3d_entropy_enc *ent = dct3d_entropy_enc_create(width, height, depth, out);
     int status = 0;
-    if (!raster || !q || !ent) {
+    if (!raster || (host_eg ? !q : !eg) || !ent) {
         printf("Out of memory\n");
         status = 1;
     }
@@ -67,24 +73,52 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
         const size_t want = stack_px * nb;
         while (got < want && (r = fread(raster + got, 1, want - got, in)) > 0) got += r;
         if (got < want) memset(raster + got, 0, want - got);
-        rc = dct3d_encode_stacks(ctx, raster, width, height, nb, q, NULL);
-        if (rc) {
-            printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
-            status = 1;
-            break;
-        }
-        for (int s = 0; s < nb; s++) {
-            if (dct3d_entropy_enc_push(ent, q + stack_px * s, s0 + s == n_stacks - 1)) {
+        const int last = s0 + nb == n_stacks;
+        if (host_eg) {  /* quantised ints over PCIe, Exp-Golomb on the host (the reference's split) */
+            rc = dct3d_encode_stacks(ctx, raster, width, height, nb, q, NULL);
+            if (rc) {
+                printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
+                status = 1;
+                break;
+            }
+            for (int s = 0; s < nb; s++) {
+                if (dct3d_entropy_enc_push(ent, q + stack_px * s, s0 + s == n_stacks - 1)) {
+                    printf("Error in the entropy coder\n");
+                    status = 1;
+                    break;
+                }
+            }
+        } else {  /* DCT + quantisation + diagonal order + Exp-Golomb on the device; the stream over PCIe */
+            uint8_t cb;
+            int cbits;
+            uint64_t tb = 0;
+            dct3d_entropy_enc_carry(ent, &cb, &cbits);
+            rc = dct3d_encode_eg(ctx, raster, width, height, nb, cb, cbits, &tb);
+            const size_t nbytes = (size_t)((tb + 7) / 8);
+            if (!rc && nbytes > eg_cap) {
+                free(eg);
+                eg_cap = nbytes + nbytes / 4;
+                eg = (unsigned char *)malloc(eg_cap);
+                if (!eg) rc = DCT3D_ENOMEM;
+            }
+            if (!rc) rc = dct3d_eg_fetch(ctx, eg, nbytes);
+            if (rc) {
+                printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
+                status = 1;
+                break;
+            }
+            if (dct3d_entropy_enc_push_stream(ent, eg, tb, last)) {
                 printf("Error in the entropy coder\n");
                 status = 1;
                 break;
             }
-            printf("Frames processed: %d\n", (s0 + s + 1) * depth);
         }
+        for (int s = 0; !status && s < nb; s++) printf("Frames processed: %d\n", (s0 + s + 1) * depth);
     }
     dct3d_entropy_enc_destroy(ent);
     free(raster);
     free(q);
+    free(eg);
     dct3d_ctx_destroy(ctx);
     fclose(in);
     if (fflush(out) || fclose(out)) status = 1;

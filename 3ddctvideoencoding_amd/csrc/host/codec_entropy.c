@@ -99,6 +99,31 @@ int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last) 
     return deflate_all(e, (const unsigned char *)e->eg, (size_t)size + 1, Z_FINISH);  /* encoder.c:292 */
 }
 
+void dct3d_entropy_enc_carry(const dct3d_entropy_enc *e, uint8_t *byte, int *bits) {
+    /* after expGolomb_freeBuffer the partial byte sits at position 0 */
+    *bits = 8 - e->st.bitPosition;
+    *byte = *bits ? (uint8_t)e->eg[e->st.bufferPosition] : 0;
+}
+
+int dct3d_entropy_enc_push_stream(dct3d_entropy_enc *e, const unsigned char *bytes, uint64_t total_bits, int is_last) {
+    if (e->finished || e->st.bufferPosition != 0) return -1;
+    const size_t complete = (size_t)(total_bits / 8);
+    const int rem = (int)(total_bits % 8);
+    if (is_last) {
+        e->finished = 1;
+        if (rem) return deflate_all(e, bytes, complete + 1, Z_FINISH);
+        /* the reference deflates bufferPosition + 1 bytes: a whole-byte stream ends with one zero byte */
+        if (complete && deflate_all(e, bytes, complete, Z_NO_FLUSH)) return -1;
+        static const unsigned char zero = 0;
+        return deflate_all(e, &zero, 1, Z_FINISH);
+    }
+    if (deflate_all(e, bytes, complete, Z_NO_FLUSH)) return -1;
+    e->eg[0] = rem ? (char)bytes[complete] : 0;
+    e->st.bitPosition = 8 - rem;
+    e->st.bufferPosition = 0;
+    return 0;
+}
+
 const unsigned char *dct3d_entropy_enc_memory(const dct3d_entropy_enc *e, size_t *len) {
     if (len) *len = e->mem_len;
     return e->mem;

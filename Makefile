@@ -14,7 +14,7 @@ OBJ     := build/obj
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function -Iinclude
 CFLAGS   := -O2 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude -std=c11 -D_GNU_SOURCE
 
-DEV_SRCS  := $(CSRC)/dct3d_kernels.hip $(CSRC)/dct3d_kernels_f.hip
+DEV_SRCS  := $(CSRC)/dct3d_kernels.hip $(CSRC)/dct3d_kernels_f.hip $(CSRC)/dct3d_eg.hip
 HOST_SRCS := $(CSRC)/dct3d_plan.cpp $(CSRC)/dct3d_runtime.cpp
 HDRS      := $(wildcard $(CSRC)/*.h) include/dct3d.h
 CODEC_SRCS := $(wildcard $(CSRC)/host/*.c)

@@ -111,8 +111,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # one process per GPU over RCCL ("nccl").  DCT3D_BENCH_BACKEND=gloo rehearses the N>1 flow with
+        # several ranks on fewer GPUs (ranks are mapped onto the visible devices round-robin).
+        backend = os.environ.get("DCT3D_BENCH_BACKEND", "nccl")
+        dev_idx = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_idx)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()

@@ -56,8 +56,9 @@ extern "C" {
 #define DCT3D_EDEVICE 2     /* no such HIP device, or a HIP runtime error */
 #define DCT3D_ENOMEM 3      /* device or host allocation failed */
 #define DCT3D_EKERNEL 4     /* a kernel launch failed */
+#define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written to it) */
 
-#define DCT3D_ABI_VERSION 1
+#define DCT3D_ABI_VERSION 2
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -163,6 +164,33 @@ int dct3d_fill_synthetic_dev(dct3d_ctx *ctx, uint8_t *d_frames, int width, int h
  * mode 1: copy n_px bytes; mode 2: write 4*n_px bytes; mode 3: read n_px bytes; modes 4/5: copy /
  * write with plain (temporal) stores.  n_px % 16 == 0. */
 int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, size_t n_px, int mode);
+
+/* ---- Exp-Golomb stage on the device -----------------------------------------
+ * Replaces applyExpGolombCoding (encoder.c:60-71) over expGolomb_writeValue (ExpGolomb.c:32-64) /
+ * ExpGolombWriter.java:19-49: the signed order-0 Exp-Golomb stream of n_cubes consecutive cube-major
+ * int32 cubes, each in diagonal-slice order (cubeUtils_diagonalSlices, CubeUtils.c:5-46), MSB first,
+ * continuing a stream whose partial byte holds `carry_byte` with `carry_bits` (0..7) bits used (the
+ * byte the reference carries from stack to stack, expGolomb_freeBuffer, ExpGolomb.c:112-130).
+ * d_out (device, 4-byte aligned, out_cap bytes) receives ceil(total_bits / 32) little-endian words,
+ * i.e. the stream bytes followed by zero padding; *total_bits = carry_bits + the bits written.
+ * Values must satisfy |v| < 2^30 (quantised 8-bit content stays below 2^13), else DCT3D_EINVAL.
+ * DCT3D_ENOSPC when out_cap is too small (*total_bits is still set; d_out is untouched).
+ * Synchronises the context stream (the total is read back). */
+int dct3d_eg_encode_dev(dct3d_ctx *ctx, const int32_t *d_q, uint64_t n_cubes, uint8_t carry_byte, int carry_bits,
+                        uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
+
+/* Host raster in, Exp-Golomb stream kept on the device: encoder.c:228-296 up to (not including) the
+ * deflate -- readCubes + DCT + quantisation + applyExpGolombCoding for n_stacks stacks, one H2D copy
+ * of the raw bytes.  *total_bits as above; fetch the bytes with dct3d_eg_fetch. */
+int dct3d_encode_eg(dct3d_ctx *ctx, const uint8_t *raster, int width, int height, int n_stacks, uint8_t carry_byte,
+                    int carry_bits, uint64_t *total_bits);
+
+/* Copies the first `nbytes` bytes of the last dct3d_encode_eg stream to host memory. */
+int dct3d_eg_fetch(dct3d_ctx *ctx, uint8_t *out, uint64_t nbytes);
+
+/* Diagonal-slice order of a bw x bh x bd cube (CubeUtils.c:5-46): out[i] = x + bw*y + bw*bh*z of the
+ * i-th position (introspection / tests). */
+int dct3d_diagonal_order(int bw, int bh, int bd, uint16_t *out);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import numpy as np
+
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -40,8 +42,21 @@ def test_codec_header_symbols_exported(pkg, header):
 
 
 def test_library_loads_and_reports_version(pkg):
-    assert pkg.lib().dct3d_abi_version() == 1
+    import re
+    hdr = open(os.path.join(REPO, "include", "dct3d.h")).read()
+    assert pkg.lib().dct3d_abi_version() == int(re.search(r"#define DCT3D_ABI_VERSION (\d+)", hdr).group(1))
     assert pkg.strerror(0) == "ok" and pkg.strerror(1) == "invalid argument"
+    assert pkg.strerror(pkg.DCT3D_ENOSPC) == "output buffer too small"
+
+
+def test_diagonal_order_matches_oracle(pkg, oracle):
+    """The device Exp-Golomb stage's order table == the oracle's CubeUtils restatement (itself pinned
+    against the reference's cubeUtils_diagonalSlices in test_oracle.py)."""
+    for d in (8, 4):
+        pos = oracle.diagonal_slices(8, 8, d)
+        assert np.array_equal(pkg.diagonal_order(8, 8, d), pos[:, 0] + 8 * pos[:, 1] + 64 * pos[:, 2])
+    with pytest.raises(pkg.Dct3dError):
+        pkg.diagonal_order(8, 8, 5)
 
 
 def test_argument_validation_without_device(pkg):

@@ -12,8 +12,12 @@ from test_host_codec import reference_entropy_encode
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("host_eg,batch", [("0", "2"), ("1", "2"), ("0", "1"), ("0", "16")])
 @pytest.mark.parametrize("w,h,frames,kind", [(64, 64, 16, "ramp"), (320, 240, 24, "uniform"), (64, 48, 12, "ramp")])
-def test_cli_encode_decode(pkg, plan8, tmp_path, w, h, frames, kind):
+def test_cli_encode_decode(pkg, plan8, tmp_path, w, h, frames, kind, host_eg, batch):
+    """host_eg "0": DCT + quantisation + Exp-Golomb on the device, one deflate call per batch;
+    "1": the reference's split (ints over PCIe, Exp-Golomb on the host, one deflate call per stack).
+    Both must give the reference encoder's bytes."""
     fr = pkg.synthetic.frames(w, h, frames, kind=kind)
     n_stacks = (frames + 7) // 8
     padded = np.zeros((n_stacks * 8, h, w), np.uint8)
@@ -21,7 +25,7 @@ def test_cli_encode_decode(pkg, plan8, tmp_path, w, h, frames, kind):
     raw = tmp_path / "in.raw"
     raw.write_bytes(fr.tobytes())
     binf, outf = tmp_path / "out.bin", tmp_path / "out.raw"
-    env = dict(os.environ, DCT3D_CODEC_BATCH="2")    # exercise several device batches
+    env = dict(os.environ, DCT3D_CODEC_BATCH=batch, DCT3D_CODEC_HOST_EG=host_eg)
     r = subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), "1"],
                        capture_output=True, text=True, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
