@@ -9,11 +9,11 @@
 // Placement of variable-length codes without a serial cursor:
 //   eg_len_kernel     one wave per cube: bits of the cube (sum of 2n - 1)
 //   scan kernels      64-bit exclusive prefix sum over cubes (reduce / top / apply), plus the total
-//   eg_zero_kernel    clears the output words and seeds word 0 with the carried partial byte
-//   eg_write_kernel   one wave per cube: lane-level exclusive scan of code lengths, codes OR-ed into
-//                     a wave-private LDS image aligned to the cube's first output word, stored as
-//                     stream-order words (byte-swapped); the two words a cube may share with its
-//                     neighbours are merged with atomicOr, the interior words are plain stores.
+//   eg_write_kernel   waves walk the cubes (next cube prefetched): lane-level exclusive scan of code
+//                     lengths, codes OR-ed into a wave-private LDS image aligned to the cube's first
+//                     output word, stored as stream-order words (byte-swapped); interior words are
+//                     plain stores, the first and last word go to head / tail
+//   eg_stitch_kernel  merges the words shared by neighbouring cubes (and the carried partial byte)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -26,7 +26,6 @@ namespace {
 constexpr int kEgBlock = 256;
 constexpr int kEgWaves = kEgBlock / 64;
 constexpr int kScanChunk = 4096;              // cubes per scan block (16 per thread)
-constexpr int kEgMaxWords = 64 * 8 * 63 / 32 + 2;  // worst cube: 512 codes of 63 bits, plus alignment
 
 // code of one value: returns the n-bit value (v <= 0 -> -2v, else 2v - 1, plus one); *width = 2n - 1.
 // Valid for |v| < 2^30 (quantised 8-bit content stays below 2^13); flags anything larger.
@@ -141,75 +140,119 @@ __global__ __launch_bounds__(kEgBlock) void eg_scan_apply_kernel(EgParams P) {
     }
 }
 
-// clears the words the stream will occupy; word 0 keeps the carried partial byte (stream byte 0)
-__global__ __launch_bounds__(kEgBlock) void eg_zero_kernel(EgParams P) {
-    if (P.status[1] != 0) return;
-    const uint64_t words = (P.status[0] + 31) / 32;
-    for (uint64_t w = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x; w < words; w += (uint64_t)gridDim.x * kEgBlock)
-        P.out[w] = w == 0 ? (uint32_t)(P.carry_byte & (0xFF00u >> P.carry_bits)) : 0u;
+// OR of one code into a word image: the n-bit value ends at stream bit e (exclusive, relative to
+// word 0 of the image); at most two words
+template <class OrFn>
+__device__ __forceinline__ void put_code(uint32_t code, int width, uint32_t e, OrFn&& or_word) {
+    const uint32_t n = ((uint32_t)width + 1) >> 1;
+    const uint32_t kl = (e - 1) >> 5;
+    const uint32_t r = e - 32 * kl;  // 1..32 bits of the value in word kl
+    or_word(kl, code << (32 - r));
+    if (n > r) or_word(kl - 1, code >> r);
 }
 
+// Each wave walks cubes g = wave_id, wave_id + n_waves, ... with the next cube's values and offset
+// prefetched while the current one is packed.  A cube's words are assembled in a 256-word LDS image
+// (8,160 bits: 16x what quantised content needs; larger cubes, up to 512 x 63 bits, take several
+// windows).  Interior words are plain stores; the first and the last word, which the cube may share
+// with its neighbours, go to head[g] / tail[g] for eg_stitch_kernel -- no global atomics, and every
+// output word is written exactly once (no zero fill).  A cube has >= 512 bits (>= 16 words), so a
+// word is shared by at most two cubes.
+constexpr int kImgWords = 256;
 template <int D>
 __global__ __launch_bounds__(kEgBlock) void eg_write_kernel(EgParams P) {
-    constexpr int CS = 64 * D, PER = CS / 64;
+    constexpr int CS = 64 * D, PER = CS / 64, V4 = PER / 4;
     __shared__ int32_t sq[kEgWaves][CS];
-    __shared__ uint32_t img[kEgWaves][kEgMaxWords];
+    __shared__ uint32_t img[kEgWaves][kImgWords];
     if (P.status[1] != 0) return;  // capacity or range failure: nothing is written
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t g = (uint64_t)blockIdx.x * kEgWaves + wave;
+    const uint64_t n_waves = (uint64_t)gridDim.x * kEgWaves;
+    uint64_t g = (uint64_t)blockIdx.x * kEgWaves + wave;
     if (g >= P.n_cubes) return;
-    // stage the cube (coalesced), then read it in diagonal-slice order
-    const int32_t* q = P.q + g * CS;
+    uint16_t dg[PER];
 #pragma unroll
-    for (int i = 0; i < PER; i += 4) *(int4*)&sq[wave][(i / 4) * 256 + lane * 4] = *(const int4*)(q + (i / 4) * 256 + lane * 4);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t code[PER];
-    int width[PER];
-    bool bad = false;
-    uint32_t lbits = 0;
+    for (int i = 0; i < PER; i++) dg[i] = P.diag[lane * PER + i];
+    int4 nxt[V4];
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        code[i] = eg_code(sq[wave][P.diag[lane * PER + i]], width[i], bad);
-        lbits += (uint32_t)width[i];
-    }
-    // exclusive scan of the lanes' bit counts (stream order = lane order)
-    uint32_t incl = lbits;
+    for (int i = 0; i < V4; i++) nxt[i] = *(const int4*)(P.q + g * CS + i * 256 + lane * 4);
+    uint64_t nxt_off = P.off[g];
+    for (; g < P.n_cubes; g += n_waves) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    const uint64_t start = P.off[g];
-    const uint32_t s0 = (uint32_t)(start & 31);
-    const uint64_t w0 = start >> 5;
-    const uint32_t nwords = (s0 + total + 31) >> 5;
-    for (uint32_t w = lane; w < nwords; w += 64) img[wave][w] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t pos = s0 + incl - lbits;  // stream bit of this lane's first code, relative to word w0
+        for (int i = 0; i < V4; i++) *(int4*)&sq[wave][i * 256 + lane * 4] = nxt[i];
+        const uint64_t start = nxt_off;
+        const uint64_t gn = g + n_waves;
+        if (gn < P.n_cubes) {  // next cube's values and offset in flight while this one is packed
 #pragma unroll
-    for (int i = 0; i < PER; i++) {
-        // the value occupies the last n bits of the code: stream bits [pos + width - n, pos + width)
-        const uint32_t e = pos + (uint32_t)width[i];
-        const uint32_t n = ((uint32_t)width[i] + 1) >> 1;
-        const uint32_t kl = (e - 1) >> 5;
-        const uint32_t r = e - 32 * kl;  // 1..32 bits of the value in word kl
-        atomicOr(&img[wave][kl], r == 32 ? code[i] : code[i] << (32 - r));
-        if (n > r) atomicOr(&img[wave][kl - 1], code[i] >> r);
-        pos = e;
+            for (int i = 0; i < V4; i++) nxt[i] = *(const int4*)(P.q + gn * CS + i * 256 + lane * 4);
+            nxt_off = P.off[gn];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t code[PER];
+        int width[PER];
+        bool bad = false;
+        uint32_t lbits = 0;
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            code[i] = eg_code(sq[wave][dg[i]], width[i], bad);
+            lbits += (uint32_t)width[i];
+        }
+        uint32_t incl = lbits;  // exclusive scan of the lanes' bit counts (stream order = lane order)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t s0 = (uint32_t)(start & 31);
+        const uint64_t w0 = start >> 5;
+        const uint32_t nwords = (s0 + total + 31) >> 5;
+        const uint32_t pos0 = s0 + incl - lbits;  // stream bit of this lane's first code, relative to w0
+        for (uint32_t win = 0; win < nwords; win += kImgWords) {
+            const uint32_t nw = min(nwords - win, (uint32_t)kImgWords);
+            for (uint32_t w = lane; w < nw; w += 64) img[wave][w] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t pos = pos0;
+#pragma unroll
+            for (int i = 0; i < PER; i++) {
+                pos += (uint32_t)width[i];
+                put_code(code[i], width[i], pos, [&](uint32_t k, uint32_t v) {
+                    if (k - win < nw) atomicOr(&img[wave][k - win], v);  // unsigned: k >= win
+                });
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t w = lane; w < nw; w += 64) {
+                const uint32_t gw = win + w;
+                const uint32_t v = __builtin_bswap32(img[wave][w]);  // stream order -> memory byte order
+                if (gw == 0) P.head[g] = v;
+                else if (gw == nwords - 1) P.tail[g] = v;
+                else P.out[w0 + gw] = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // img / sq reuse
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t w = lane; w < nwords; w += 64) {
-        const uint32_t v = __builtin_bswap32(img[wave][w]);  // stream order -> memory byte order
-        if (w == 0 || w == nwords - 1) atomicOr(&P.out[w0 + w], v);  // shared with a neighbour
-        else P.out[w0 + w] = v;
-    }
+}
+
+// thread per cube: the first word of cube g = its head | the previous cube's tail when they share the
+// word (| the carried partial byte for g = 0); the last word (tail) unless the next cube shares it
+__global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
+    if (P.status[1] != 0) return;
+    const uint64_t g = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
+    if (g >= P.n_cubes) return;
+    const uint64_t start = P.off[g], end = start + P.bits[g];
+    const uint64_t w0 = start >> 5, wl = (end - 1) >> 5;
+    uint32_t first = P.head[g];
+    if (g == 0) first |= P.carry_byte & (0xFF00u >> P.carry_bits);  // stream byte 0 = memory byte 0
+    else if (((start - 1) >> 5) == w0) first |= P.tail[g - 1];
+    P.out[w0] = first;
+    if (g + 1 == P.n_cubes || (end >> 5) != wl) P.out[wl] = P.tail[g];
 }
 
 }  // namespace
@@ -224,9 +267,16 @@ int launch_eg_encode(int D, const EgParams& P, hipStream_t st) {
     hipLaunchKernelGGL(eg_scan_reduce_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
     hipLaunchKernelGGL(eg_scan_top_kernel, dim3(1), dim3(1024), 0, st, P, (uint32_t)n_chunks);
     hipLaunchKernelGGL(eg_scan_apply_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
-    hipLaunchKernelGGL(eg_zero_kernel, dim3(2048), dim3(kEgBlock), 0, st, P);
-    if (D == 8) hipLaunchKernelGGL(eg_write_kernel<8>, dim3((uint32_t)cube_blocks), dim3(kEgBlock), 0, st, P);
-    else hipLaunchKernelGGL(eg_write_kernel<4>, dim3((uint32_t)cube_blocks), dim3(kEgBlock), 0, st, P);
+    static int wgrid = -1;
+    if (wgrid < 0) {  // persistent-style writer: 8 blocks (32 waves) per CU
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        wgrid = cus * 8;
+    }
+    const uint32_t wblocks = (uint32_t)(cube_blocks < (uint64_t)wgrid ? cube_blocks : (uint64_t)wgrid);
+    if (D == 8) hipLaunchKernelGGL(eg_write_kernel<8>, dim3(wblocks), dim3(kEgBlock), 0, st, P);
+    else hipLaunchKernelGGL(eg_write_kernel<4>, dim3(wblocks), dim3(kEgBlock), 0, st, P);
+    hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -85,6 +85,8 @@ struct EgParams {
     uint64_t* off;             // [n_cubes] stream bit offset of each cube (carry included)
     uint64_t* bsum;            // [n_chunks] chunk sums -> chunk offsets
     uint64_t* status;          // [0] total bits (carry included), [1] flags: 1 capacity, 2 value range
+    uint32_t* head;            // [n_cubes] first output word of each cube (memory byte order)
+    uint32_t* tail;            // [n_cubes] last output word of each cube
     uint32_t* out;             // output words (memory byte order), capacity out_cap_words
     uint64_t out_cap_words;
     uint32_t carry_bits, carry_byte;

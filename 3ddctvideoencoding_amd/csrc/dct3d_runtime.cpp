@@ -67,7 +67,7 @@ struct dct3d_ctx {
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
-    DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q;
+    DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
     uint64_t eg_last_bytes = 0;
 };
 
@@ -191,7 +191,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
                       &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
-                      &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q})
+                      &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -530,6 +530,7 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     int rc = c->d_eg_bits.grow(n_cubes * sizeof(uint32_t));
     if (!rc) rc = c->d_eg_off.grow(n_cubes * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t));
+    if (!rc) rc = c->d_eg_ht.grow(2 * n_cubes * sizeof(uint32_t));
     if (rc) return rc;
     if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     EgParams P;
@@ -540,6 +541,8 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     P.off = (uint64_t*)c->d_eg_off.p;
     P.bsum = (uint64_t*)c->d_eg_bsum.p;
     P.status = (uint64_t*)c->d_eg_status.p;
+    P.head = (uint32_t*)c->d_eg_ht.p;
+    P.tail = (uint32_t*)c->d_eg_ht.p + n_cubes;
     P.out = d_out;
     P.out_cap_words = out_cap / 4;
     P.carry_bits = (uint32_t)carry_bits;

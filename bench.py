@@ -34,6 +34,8 @@ CONFIGS = {
     "c4_encode_4k": (3840, 2160, 8, 8, "encode"),
     "c5_encode_1080p_d4": (1920, 1080, 4, 128, "encode"),
     "c6_decode_1080p_d4": (1920, 1080, 4, 128, "decode"),
+    # encode to the Exp-Golomb stream: DCT + quantise + diagonal order + EG per step
+    "c7_encode_eg_1080p": (1920, 1080, 8, 128, "encode_eg"),
 }
 
 
@@ -138,12 +140,25 @@ def main():
     # each rank encodes different content (its own slice of one long synthetic video)
     ctx.fill_synthetic_dev(frames, width, height, stacks * depth, frame0=rank * stacks * depth, kind=a.kind)
     q = torch.empty((n_cubes * cs,), dtype=torch.int32, device="cuda")
+    eg_info = {}
     if direction == "decode":
         ctx.encode_stacks_dev(frames, width, height, stacks, q)  # input of the decode = encoder output
         out = torch.empty_like(frames)
 
         def step():
             ctx.decode_stacks_dev(q, width, height, stacks, out)
+    elif direction == "encode_eg":
+        eg_cap = n_cubes * cs  # 8 bits per value: far above what quantised content needs
+        eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
+        eg_ev = []
+
+        def step():
+            ctx.encode_stacks_dev(frames, width, height, stacks, q)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            eg_info["bits"] = ctx.eg_encode_dev(q, n_cubes, eg_out, eg_cap)  # synchronises (total read back)
+            e1.record()
+            eg_ev.append((e0, e1))
     else:
         def step():
             ctx.encode_stacks_dev(frames, width, height, stacks, q)
@@ -188,11 +203,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f64" if direction == "decode" else "f32",
         "data": "synthetic",
         "config": {
             "workload": f"{width}x{height} grayscale, {depth}-frame stacks, "
-                        f"{'forward 3D DCT + quantise' if direction == 'encode' else 'dequantise + inverse 3D DCT'}"
+                        f"{ {'encode': 'forward 3D DCT + quantise', 'decode': 'dequantise + inverse 3D DCT', 'encode_eg': 'forward 3D DCT + quantise + diagonal order + Exp-Golomb stream'}[direction] }"
                         f" ({unit_name} cubes), {stacks} device-resident stacks per GPU per step",
             "name": a.config,
             "stacks_per_gpu": stacks,
@@ -207,7 +222,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None,
-            "kernel": "encode_kernel" if direction == "encode" else "decode_kernel",
+            "kernel": "decode_kernel" if direction == "decode" else "encode_kernel",
             "kernel_ms": kernel_ms,
             "fixup_ms": fixup_ms,
             "bytes_per_cube": bytes_per_cube,
@@ -216,6 +231,10 @@ def main():
         "flagged_units_last_step": st["n_flagged"],
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,
+        "eg_stage": None if direction != "encode_eg" else {
+            "ms_per_step": sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps,
+            "bits_per_value": eg_info["bits"] / (n_cubes * cs),
+            "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

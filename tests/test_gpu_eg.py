@@ -62,6 +62,9 @@ def test_eg_random_values_and_chunk_edges(pkg, oracle, gpu_ctx8, n_cubes):
     big = rng.random(q.shape) < 0.002
     q[big] = rng.integers(-(2**30) + 1, 2**30, size=int(big.sum()))
     q.reshape(-1)[:4] = [2**30 - 1, -(2**30) + 1, 0, 1]
+    if n_cubes > 2:   # cubes whose codes exceed the writer's LDS image (8,160 bits): global-atomic path
+        q[1] = rng.integers(2**28, 2**30, size=(8, 8, 8)) * rng.choice([-1, 1], size=(8, 8, 8))
+        q[2, :4] = rng.integers(-(2**20), 2**20, size=(4, 8, 8))
     exp, ebits = _expected(oracle, pkg, q, 8)
     got, tb, _ = _gpu_stream(gpu_ctx8, q)
     assert tb == ebits and got == exp

@@ -1,0 +1,39 @@
+"""End-to-end codec timing (run on the GPU box): the reference-compatible CLI on a synthetic 1080p raw
+file, Exp-Golomb on the host (the reference's split: quantised ints over PCIe) vs on the device (only
+the stream crosses PCIe); both must write the same .bin.  Prints one JSON line."""
+import importlib, json, os, subprocess, sys, tempfile, time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+pkg = importlib.import_module("3ddctvideoencoding_amd")
+
+W, H = 1920, 1080
+F = int(os.environ.get("E2E_FRAMES", "64"))
+tmp = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+raw = os.path.join(tmp, "in.raw")
+with open(raw, "wb") as f:
+    for s in range(0, F, 8):
+        f.write(pkg.synthetic.frames(W, H, min(8, F - s), kind="ramp", frame0=s).tobytes())
+res = {"frames": F, "width": W, "height": H, "raw_MB": W * H * F / 1e6}
+bins = {}
+for mode in ("1", "0"):
+    env = dict(os.environ, DCT3D_CODEC_HOST_EG=mode)
+    out = os.path.join(tmp, f"out{mode}.bin")
+    t0 = time.perf_counter()
+    r = subprocess.run([pkg.CLI_PATH, "encode", raw, out, str(W), str(H), str(F), "1"], capture_output=True, text=True,
+                       env=env)
+    dt = time.perf_counter() - t0
+    assert r.returncode == 0, r.stdout + r.stderr
+    bins[mode] = open(out, "rb").read()
+    res["encode_host_eg_s" if mode == "1" else "encode_device_eg_s"] = dt
+res["bin_identical"] = bins["0"] == bins["1"]
+res["bin_MB"] = len(bins["0"]) / 1e6
+t0 = time.perf_counter()
+r = subprocess.run([pkg.CLI_PATH, "decode", os.path.join(tmp, "out0.bin"), os.path.join(tmp, "dec.raw"), str(W), str(H),
+                    str(F), "1"], capture_output=True, text=True)
+res["decode_s"] = time.perf_counter() - t0
+assert r.returncode == 0, r.stdout + r.stderr
+res["encode_device_eg_fps"] = F / res["encode_device_eg_s"]
+res["encode_host_eg_fps"] = F / res["encode_host_eg_s"]
+res["decode_fps"] = F / res["decode_s"]
+print(json.dumps(res))

@@ -7,7 +7,8 @@ ARGS=${BENCH_ARGS:-"--steps 6 --warmup 2 --no-cpu-baseline --no-ceiling"}
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU" \
-           "SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS"; do
+           "SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_LDS" \
+           ${SQ_EXTRA:+"$SQ_EXTRA"}; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp -d $OUT/p$i -o p$i --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/p$i.log; exit $rc; }
