@@ -77,6 +77,24 @@ def cpu_baseline(width, height, depth, budget_s, kind):
                       f"DCT.run + Encoder quantisation, {threads} threads, {t_total:.1f} s"}
 
 
+def pmc_traffic(config: str, kernel: str, depth: int):
+    """HBM bytes per launch of `kernel` from the PMC summary of this config (tools/gpu_pmc.sh ->
+    profiles/pmc/<config>.csv): FETCH_SIZE (KB, x2 -- on gfx950 it counts half of a wide coalesced
+    stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE (KB).  None when no summary was collected."""
+    import csv
+    path = os.path.join(REPO, "profiles", "pmc", f"{config}.csv")
+    if not os.path.exists(path):
+        return None, None
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        name = r["kernel"]
+        if f"{kernel}<{depth}" in name and "fixup" not in name:
+            vals[r["counter"]] = float(r["avg_per_launch_raw"])
+    if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
+        return None, None
+    return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
+
+
 def measure_ceiling(ctx, torch, frames, q, reps):
     """Achievable HBM rates on this device for the path's traffic mix, same buffers, same stream:
     mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only."""
@@ -191,6 +209,8 @@ def main():
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
     fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
     achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
+    kname = "decode_kernel" if direction == "decode" else "encode_kernel"
+    traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
         "metric": "8×8×8 cubes/s (encode DCT+quant) on 1080p×8-frame stacks; % HBM roofline at 1/2/4/8 GPUs",
@@ -221,8 +241,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
-            "kernel": "decode_kernel" if direction == "decode" else "encode_kernel",
+            "traffic": traffic,  # HBM bytes per launch (PMC), compare with algorithmic_bytes
+            "traffic_source": traffic_src,
+            "algorithmic_bytes": n_cubes * bytes_per_cube,
+            "kernel": kname,
             "kernel_ms": kernel_ms,
             "fixup_ms": fixup_ms,
             "bytes_per_cube": bytes_per_cube,
