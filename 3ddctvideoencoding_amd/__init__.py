@@ -26,7 +26,7 @@ CLI_PATH = os.path.join(LIB_DIR, "dct3d_codec")
 REPO_DIR = os.path.dirname(PKG_DIR)
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
-DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC = 0, 1, 2, 3, 4, 5
+DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -36,6 +36,8 @@ ABI_SYMBOLS = (
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
     "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev",
+    "dct3d_eg_encode_dev", "dct3d_encode_eg", "dct3d_eg_fetch", "dct3d_diagonal_order",
+    "dct3d_eg_decode_dev", "dct3d_decode_eg",
 )
 
 
@@ -101,6 +103,8 @@ def lib() -> C.CDLL:
         L.dct3d_encode_eg.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, C.POINTER(u64)]
         L.dct3d_eg_fetch.argtypes = [vp, vp, u64]
         L.dct3d_diagonal_order.argtypes = [i32, i32, i32, vp]
+        L.dct3d_eg_decode_dev.argtypes = [vp, vp, u64, u64, u64, vp, C.POINTER(u64)]
+        L.dct3d_decode_eg.argtypes = [vp, vp, u64, i32, i32, i32, i32, vp, C.POINTER(u64)]
         _lib = L
     return _lib
 
@@ -292,6 +296,24 @@ class Context:
         out = np.empty(eg_stream_bytes(tb.value), np.uint8)
         _check(lib().dct3d_eg_fetch(self._h, _ptr(out) if out.size else None, out.size), "dct3d_eg_fetch")
         return out.tobytes(), tb.value
+
+    def eg_decode_dev(self, d_bytes, nbytes: int, start_bit: int, n_cubes: int, d_q) -> int:
+        """Device Exp-Golomb stream (4-byte aligned) -> n_cubes cube-major int32 cubes; returns the bit
+        after the last value.  Dct3dError(DCT3D_ENODATA) if the stream is too short."""
+        eb = C.c_uint64(0)
+        _check(lib().dct3d_eg_decode_dev(self._h, _tptr(d_bytes), nbytes, start_bit, n_cubes, _tptr(d_q), C.byref(eb)),
+               "dct3d_eg_decode_dev")
+        return eb.value
+
+    def decode_eg(self, stream: bytes, width: int, height: int, n_stacks: int, start_bit: int = 0):
+        """Exp-Golomb stream bytes (from bit start_bit, 0..7) -> (u8 frames [n_stacks*bd, H, W], end bit):
+        entropy decode + dequantise + IDCT on the device."""
+        b = np.frombuffer(stream, np.uint8)
+        out = np.empty((n_stacks * self.bd, height, width), np.uint8)
+        eb = C.c_uint64(0)
+        _check(lib().dct3d_decode_eg(self._h, _ptr(b) if b.size else None, b.size, start_bit, width, height, n_stacks,
+                                     _ptr(out), C.byref(eb)), "dct3d_decode_eg")
+        return out, eb.value
 
     def fill_synthetic_dev(self, d_frames, width: int, height: int, n_frames: int,
                            seed: int = synthetic.DEFAULT_SEED, frame0: int = 0, kind: str = "ramp") -> None:

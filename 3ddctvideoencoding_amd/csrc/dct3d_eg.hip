@@ -255,6 +255,125 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
     if (g + 1 == P.n_cubes || (end >> 5) != wl) P.out[wl] = P.tail[g];
 }
 
+// =================================================================================================
+// Decode: the inverse of the stream above (expGolomb_readValue, ExpGolomb.c:66-110 /
+// ExpGolombReader.java:19-63; Decoder.java:78-96 places value i of a cube at diagonal position i).
+// Self-synchronising parallel decode: the stream is cut into kChunkBits chunks, one thread each.
+//   sync pass k   thread t parses codewords from its start (k = 0: the chunk's first bit; later: the
+//                 previous pass's exit of chunk t - 1) until it passes the chunk's end; exit = the
+//                 first codeword boundary at or past the end.  Repeated until no exit changes: chunk 0
+//                 starts at the true first bit, so by induction every start is then a true boundary.
+//                 Exp-Golomb parses resynchronise within a few codewords, so two passes are typical.
+//   scan          value index of each chunk's first codeword
+//   write pass    each chunk parsed once more from its (true) start; value idx goes to cube idx / cs,
+//                 diagonal position idx % cs; the end bit of value n_values - 1 is recorded.
+// A parse that meets 32 zero bits (no valid code has more than 30 leading zeros) ends "invalid":
+// in a true parse inside the wanted values that means a corrupt stream.
+constexpr uint64_t kChunkBits = 1024;
+constexpr uint64_t kNoExit = ~0ull;
+
+struct BitReader {
+    const uint32_t* w;
+    uint64_t nw;
+    uint64_t next;   // next word to load
+    uint64_t buf;    // left-aligned bits [pos, pos + avail)
+    int avail;
+    uint64_t pos;
+    __device__ __forceinline__ uint32_t word(uint64_t k) const { return k < nw ? __builtin_bswap32(w[k]) : 0u; }
+    __device__ __forceinline__ void seek(uint64_t p) {
+        pos = p;
+        const uint64_t k = p >> 5;
+        const int sh = (int)(p & 31);
+        buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+        avail = 64 - sh;
+        next = k + 2;
+    }
+    // one codeword: false when 32 zero bits come first (invalid); *code = the (z+1)-bit value
+    __device__ __forceinline__ bool get(uint32_t& code) {
+        if (avail <= 32) {
+            buf |= (uint64_t)word(next++) << (32 - avail);
+            avail += 32;
+        }
+        const int z = buf ? __clzll((long long)buf) : 64;
+        if (z >= 32) return false;
+        const int width = 2 * z + 1;
+        if (width <= avail) {
+            code = (uint32_t)(buf >> (64 - width));
+            buf <<= width;
+            avail -= width;
+            pos += (uint64_t)width;
+        } else {  // a long code straddling the buffer: read it at its absolute position
+            const uint64_t k = pos >> 5;
+            const int sh = (int)(pos & 31);
+            const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+            const uint64_t win = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
+            code = (uint32_t)(win >> (64 - width));
+            seek(pos + (uint64_t)width);
+        }
+        return true;
+    }
+};
+
+__device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader.java:52-62
+    const uint32_t m = code - 1u;
+    return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
+}
+
+__device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t, int iteration) {
+    if (t == 0) return P.start_bit;
+    if (iteration == 0) return P.start_bit + t * kChunkBits;
+    const uint64_t e = P.exit_in[t - 1];
+    return e == kNoExit ? P.start_bit + t * kChunkBits : e;
+}
+
+__global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration) {
+    const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
+    if (t >= P.n_chunks) return;
+    const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
+    BitReader r{P.words, P.n_words, 0, 0, 0, 0};
+    r.seek(chunk_start(P, t, iteration));
+    uint32_t n = 0, code;
+    bool invalid = false;
+    while (r.pos < end && r.pos < P.limit_bit) {
+        if (!r.get(code) || r.pos > P.limit_bit) {  // 32 zero bits, or a code running past the data
+            invalid = true;
+            break;
+        }
+        n++;
+    }
+    const uint64_t ex = invalid ? kNoExit : r.pos;
+    P.exit_out[t] = ex;
+    P.count[t] = n;
+    if (iteration > 0 && ex != P.exit_in[t]) atomicOr((unsigned int*)&P.status[0], 1u);
+}
+
+__global__ __launch_bounds__(kEgBlock) void eg_decode_write_kernel(EgDecParams P) {
+    const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
+    if (t >= P.n_chunks) return;
+    uint64_t idx = P.off[t];
+    if (idx >= P.n_values) return;
+    const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
+    BitReader r{P.words, P.n_words, 0, 0, 0, 0};
+    // the converged exits are in exit_in (the host swaps the buffers after every pass)
+    const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
+    if (s == kNoExit) {  // the true parse stopped in an earlier chunk: reported by that chunk
+        return;
+    }
+    r.seek(s);
+    uint32_t code;
+    while (idx < P.n_values && r.pos < end) {
+        const uint64_t p0 = r.pos;
+        if (p0 >= P.limit_bit || !r.get(code) || r.pos > P.limit_bit) {
+            // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
+            atomicOr((unsigned int*)&P.status[2], p0 + 32 <= P.limit_bit && r.pos <= P.limit_bit ? 1u : 2u);
+            return;
+        }
+        const uint64_t cube = idx / (uint64_t)P.cs;
+        P.q[cube * P.cs + P.diag[idx - cube * P.cs]] = eg_value(code);
+        if (++idx == P.n_values) P.status[1] = r.pos;  // the bit after the last wanted value
+    }
+}
+
 }  // namespace
 
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st) {
@@ -277,6 +396,33 @@ int launch_eg_encode(int D, const EgParams& P, hipStream_t st) {
     if (D == 8) hipLaunchKernelGGL(eg_write_kernel<8>, dim3(wblocks), dim3(kEgBlock), 0, st, P);
     else hipLaunchKernelGGL(eg_write_kernel<4>, dim3(wblocks), dim3(kEgBlock), 0, st, P);
     hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace dct3d
+
+namespace dct3d {
+
+int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st) {
+    if (P.n_chunks == 0) return 0;
+    hipLaunchKernelGGL(eg_sync_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st,
+                       P, iteration);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_eg_scan(const EgParams& P, hipStream_t st) {
+    if (P.n_cubes == 0) return 0;
+    const uint64_t n_chunks = (P.n_cubes + kScanChunk - 1) / kScanChunk;
+    hipLaunchKernelGGL(eg_scan_reduce_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
+    hipLaunchKernelGGL(eg_scan_top_kernel, dim3(1), dim3(1024), 0, st, P, (uint32_t)n_chunks);
+    hipLaunchKernelGGL(eg_scan_apply_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_eg_decode_write(const EgDecParams& P, hipStream_t st) {
+    if (P.n_chunks == 0) return 0;
+    hipLaunchKernelGGL(eg_decode_write_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock),
+                       0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

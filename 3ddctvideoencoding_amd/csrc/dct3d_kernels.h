@@ -92,8 +92,28 @@ struct EgParams {
     uint32_t carry_bits, carry_byte;
 };
 
+// Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)
+struct EgDecParams {
+    const uint32_t* words;     // stream, memory byte order
+    uint64_t n_words;
+    uint64_t start_bit, limit_bit;  // first bit of the stream, end of the available bits
+    uint64_t n_chunks;
+    uint64_t n_values;         // values wanted (n_cubes * cs)
+    int cs;
+    const uint16_t* diag;
+    uint64_t* exit_in;         // previous iteration's exits (UINT64_MAX: the parse ended invalid)
+    uint64_t* exit_out;
+    uint32_t* count;           // codewords per chunk
+    uint64_t* off;             // value index of each chunk's first codeword (scan)
+    uint64_t* status;          // [0] changed / first invalid chunk, [1] end bit, [2] flags 1 corrupt, [3] values
+    int32_t* q;                // cube-major output
+};
+
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
+int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st);
+int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
+int launch_eg_decode_write(const EgDecParams& P, hipStream_t st);
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
 int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
 int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,

@@ -68,6 +68,8 @@ struct dct3d_ctx {
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
+    // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
+    DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster;
     uint64_t eg_last_bytes = 0;
 };
 
@@ -96,6 +98,7 @@ const char* dct3d_strerror(int code) {
         case DCT3D_ENOMEM: return "out of memory";
         case DCT3D_EKERNEL: return "kernel launch failed";
         case DCT3D_ENOSPC: return "output buffer too small";
+        case DCT3D_ENODATA: return "input stream ends early";
         default: return "unknown error";
     }
 }
@@ -177,6 +180,7 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         rc = upload(c->d_diag, diag.data(), diag.size() * sizeof(uint16_t));
     }
     if (!rc) rc = c->d_eg_status.grow(16);
+    if (!rc) rc = c->d_egd_status.grow(32);
     if (rc) {
         dct3d_ctx_destroy(c);
         return rc;
@@ -191,7 +195,8 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
                       &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
-                      &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht})
+                      &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
+                      &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -612,6 +617,103 @@ int dct3d_eg_fetch(dct3d_ctx* c, uint8_t* out, uint64_t nbytes) {
     if (hipMemcpyAsync(out, c->d_eg_out.p, nbytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
+    return DCT3D_OK;
+}
+
+int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
+                        int32_t* d_q, uint64_t* end_bit) {
+    if (!c || (n_cubes && (!d_bytes || !d_q)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    const uint64_t limit = nbytes * 8;
+    if (end_bit) *end_bit = start_bit;
+    if (n_cubes == 0) return DCT3D_OK;
+    if (start_bit >= limit) return DCT3D_ENODATA;
+    const uint64_t n_chunks = (limit - start_bit + 1023) / 1024;
+    const uint64_t n_scan = (n_chunks + 4095) / 4096;
+    int rc = c->d_egd_exit.grow(2 * n_chunks * sizeof(uint64_t));
+    if (!rc) rc = c->d_eg_bits.grow(n_chunks * sizeof(uint32_t));
+    if (!rc) rc = c->d_eg_off.grow(n_chunks * sizeof(uint64_t));
+    if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
+    if (rc) return rc;
+    EgDecParams D;
+    D.words = (const uint32_t*)d_bytes;
+    D.n_words = (nbytes + 3) / 4;
+    D.start_bit = start_bit;
+    D.limit_bit = limit;
+    D.n_chunks = n_chunks;
+    D.n_values = n_cubes * (uint64_t)c->plan.cs;
+    D.cs = c->plan.cs;
+    D.diag = (const uint16_t*)c->d_diag.p;
+    uint64_t* ex[2] = {(uint64_t*)c->d_egd_exit.p, (uint64_t*)c->d_egd_exit.p + n_chunks};
+    D.count = (uint32_t*)c->d_eg_bits.p;
+    D.off = (uint64_t*)c->d_eg_off.p;
+    D.status = (uint64_t*)c->d_egd_status.p;
+    D.q = d_q;
+    // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts; two passes
+    // are the usual total); at most n_chunks + 1 passes by induction from chunk 0
+    int cur = 0;
+    for (uint64_t it = 0; it <= n_chunks + 1; it++) {
+        if (hipMemsetAsync(c->d_egd_status.p, 0, 32, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+        D.exit_in = ex[cur];
+        D.exit_out = ex[cur ^ 1];
+        if (launch_eg_sync(D, (int)(it < 2 ? it : 1), c->stream)) return DCT3D_EKERNEL;
+        cur ^= 1;
+        if (it == 0) continue;
+        uint64_t changed = 0;
+        if (hipMemcpyAsync(&changed, c->d_egd_status.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return DCT3D_EDEVICE;
+        if (!changed) break;
+        if (it == n_chunks + 1) return DCT3D_EINVAL;  // cannot happen: every pass fixes one more chunk
+    }
+    // value index of each chunk's first codeword
+    EgParams S;
+    memset(&S, 0, sizeof(S));
+    S.n_cubes = n_chunks;
+    S.bits = D.count;
+    S.off = D.off;
+    S.bsum = (uint64_t*)c->d_eg_bsum.p;
+    S.status = (uint64_t*)c->d_eg_status.p;
+    S.out_cap_words = ~0ull;
+    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
+    D.exit_in = ex[cur];  // the converged exits
+    if (launch_eg_decode_write(D, c->stream)) return DCT3D_EKERNEL;
+    uint64_t st[4] = {0, 0, 0, 0}, total[2] = {0, 0};
+    if (hipMemcpyAsync(st, c->d_egd_status.p, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(total, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    if (st[2] & 1) return DCT3D_EINVAL;
+    if ((st[2] & 2) || total[0] < D.n_values) return DCT3D_ENODATA;
+    if (end_bit) *end_bit = st[1];
+    return DCT3D_OK;
+}
+
+int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int start_bit, int w, int h, int n_stacks,
+                    uint8_t* raster, uint64_t* end_bit) {
+    if (!c || (n_stacks && (!bytes || !raster)) || start_bit < 0 || start_bit > 7) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    if (end_bit) *end_bit = (uint64_t)start_bit;
+    if (n_cubes == 0) return DCT3D_OK;
+    const size_t px = n_cubes * c->plan.cs;
+    if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3)) || (rc = c->d_eg_q.grow(px * sizeof(int32_t))) ||
+        (rc = c->d_egd_raster.grow(px)))
+        return rc;
+    if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    uint64_t eb = 0;
+    rc = dct3d_eg_decode_dev(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, (int32_t*)c->d_eg_q.p,
+                             &eb);
+    if (rc) return rc;
+    if ((rc = dct3d_decode_stacks_dev(c, (const int32_t*)c->d_eg_q.p, w, h, n_stacks, (uint8_t*)c->d_egd_raster.p)))
+        return rc;
+    if (hipMemcpyAsync(raster, c->d_egd_raster.p, px, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    if (end_bit) *end_bit = eb;
     return DCT3D_OK;
 }
 

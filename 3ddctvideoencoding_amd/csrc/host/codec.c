@@ -154,24 +154,59 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
     }
     const size_t frame = (size_t)width * height, stack_px = frame * depth;
     const int n_stacks = (frames + depth - 1) / depth;
+    /* DCT3D_CODEC_HOST_EG=1: Exp-Golomb decode on the host, ints over PCIe (the reference's split);
+     * default: the device decodes the inflated stream (dct3d_decode_eg), only the stream crosses PCIe */
+    const char *he = getenv("DCT3D_CODEC_HOST_EG");
+    const int host_eg = he && he[0] == '1';
     uint8_t *raster = (uint8_t *)malloc(stack_px * batch);
-    int32_t *q = (int32_t *)malloc(stack_px * batch * sizeof(int32_t));
+    int32_t *q = host_eg ? (int32_t *)malloc(stack_px * batch * sizeof(int32_t)) : NULL;
     dct3d_entropy_dec *ent = dct3d_entropy_dec_create(width, height, depth, in, NULL, 0);
     int status = 0;
-    if (!raster || !q || !ent) {
+    double bits_per_value = 4.0;  /* window estimate for the first batch; then the measured rate */
+    if (!raster || (host_eg && !q) || !ent) {
         printf("Out of memory\n");
         status = 1;
     }
     for (int s0 = 0; !status && s0 < n_stacks; s0 += batch) {
         const int nb = (n_stacks - s0) < batch ? (n_stacks - s0) : batch;
-        for (int s = 0; s < nb; s++)
-            if (dct3d_entropy_dec_pull(ent, q + stack_px * s)) {
+        if (host_eg) {
+            for (int s = 0; s < nb; s++)
+                if (dct3d_entropy_dec_pull(ent, q + stack_px * s)) {
+                    printf("Truncated or corrupt input stream\n");
+                    status = 1;
+                    break;
+                }
+            if (status) break;
+            rc = dct3d_decode_stacks(ctx, q, width, height, nb, raster);
+        } else {
+            const double values = (double)stack_px * nb;
+            size_t need = (size_t)(values * bits_per_value / 8 * 1.25) + 65536;
+            for (;;) {
+                const unsigned char *p;
+                size_t len;
+                int bit;
+                uint64_t eb = 0;
+                if (dct3d_entropy_dec_window(ent, need, &p, &len, &bit)) {
+                    rc = DCT3D_EINVAL;
+                    break;
+                }
+                rc = dct3d_decode_eg(ctx, p, len, bit, width, height, nb, raster, &eb);
+                if (rc == DCT3D_ENODATA && !dct3d_entropy_dec_eof(ent) && len >= need) {
+                    need *= 2;  /* the batch needs more of the stream than estimated */
+                    continue;
+                }
+                if (!rc) {
+                    dct3d_entropy_dec_consume(ent, eb);
+                    bits_per_value = (double)(eb - (uint64_t)bit) / values;
+                }
+                break;
+            }
+            if (rc == DCT3D_ENODATA || rc == DCT3D_EINVAL) {
                 printf("Truncated or corrupt input stream\n");
                 status = 1;
                 break;
             }
-        if (status) break;
-        rc = dct3d_decode_stacks(ctx, q, width, height, nb, raster);
+        }
         if (rc) {
             printf("Error running the inverse 3D DCT: %s\n", dct3d_strerror(rc));
             status = 1;

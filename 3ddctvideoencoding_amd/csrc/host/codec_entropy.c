@@ -222,6 +222,21 @@ static int refill(dct3d_entropy_dec *d, size_t need) {
     }
 }
 
+int dct3d_entropy_dec_window(dct3d_entropy_dec *d, size_t need, const unsigned char **p, size_t *len, int *bit) {
+    if (refill(d, need)) return -1;
+    *p = d->buf + d->st.bufferPosition;
+    *len = d->len - (size_t)d->st.bufferPosition;
+    *bit = 8 - d->st.bitPosition;
+    return 0;
+}
+
+void dct3d_entropy_dec_consume(dct3d_entropy_dec *d, uint64_t bits) {
+    d->st.bufferPosition += (int)(bits / 8);
+    d->st.bitPosition = 8 - (int)(bits % 8);
+}
+
+int dct3d_entropy_dec_eof(const dct3d_entropy_dec *d) { return d->zeof; }
+
 int dct3d_entropy_dec_pull(dct3d_entropy_dec *d, int32_t *q) {
     for (size_t c = 0; c < d->cubes; c++) {
         int32_t *cube = q + c * d->cs;

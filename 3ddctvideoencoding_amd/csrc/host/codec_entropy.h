@@ -36,6 +36,13 @@ dct3d_entropy_dec *dct3d_entropy_dec_create(int width, int height, int depth, FI
                                             size_t len);
 /* fills one stack of cubes (cube-major int32); returns 0, or -1 on a truncated/corrupt stream */
 int dct3d_entropy_dec_pull(dct3d_entropy_dec *d, int32_t *q);
+/* the unconsumed inflated bytes (at least `need` unless the stream ends first) and the bit of the
+ * first byte where the next code starts (0..7): the input of a device decode (dct3d_decode_eg) */
+int dct3d_entropy_dec_window(dct3d_entropy_dec *d, size_t need, const unsigned char **p, size_t *len, int *bit);
+/* consumes `bits` bits counted from the window's first byte (the window's start bit included) */
+void dct3d_entropy_dec_consume(dct3d_entropy_dec *d, uint64_t bits);
+/* 1 when the compressed input is exhausted (no more bytes will appear in the window) */
+int dct3d_entropy_dec_eof(const dct3d_entropy_dec *d);
 void dct3d_entropy_dec_destroy(dct3d_entropy_dec *d);
 
 /* whole-buffer helpers (tests): q = n_stacks stacks cube-major */

@@ -57,6 +57,7 @@ extern "C" {
 #define DCT3D_ENOMEM 3      /* device or host allocation failed */
 #define DCT3D_EKERNEL 4     /* a kernel launch failed */
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written to it) */
+#define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
 #define DCT3D_ABI_VERSION 2
 
@@ -191,6 +192,22 @@ int dct3d_eg_fetch(dct3d_ctx *ctx, uint8_t *out, uint64_t nbytes);
 /* Diagonal-slice order of a bw x bh x bd cube (CubeUtils.c:5-46): out[i] = x + bw*y + bw*bh*z of the
  * i-th position (introspection / tests). */
 int dct3d_diagonal_order(int bw, int bh, int bd, uint16_t *out);
+
+/* Inverse of the Exp-Golomb stage (expGolomb_readValue, ExpGolomb.c:66-110 / ExpGolombReader.java;
+ * Decoder.java:78-96 places value i of a cube at diagonal position i; decoder.c:210-236): decodes
+ * n_cubes cubes (n_cubes * cube_size values) from the device stream d_bytes (4-byte aligned,
+ * nbytes) starting at bit start_bit, into cube-major int32 d_q.  Parallel: self-synchronising
+ * chunks of the stream (no index is needed in the file).  *end_bit = the bit after the last value.
+ * DCT3D_ENODATA if the stream ends first, DCT3D_EINVAL if it is corrupt (a code with 32 or more
+ * leading zeros).  Synchronises the context stream. */
+int dct3d_eg_decode_dev(dct3d_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
+                        int32_t *d_q, uint64_t *end_bit);
+
+/* Host stream in, raster out: decoder.c:209-295 after the inflate -- Exp-Golomb decode, reorder,
+ * dequantisation, IDCT, clamp/truncate and writeCubes for n_stacks stacks, on the device; only the
+ * stream and the u8 frames cross PCIe.  bytes[0..nbytes) holds the stream from bit start_bit (0..7). */
+int dct3d_decode_eg(dct3d_ctx *ctx, const uint8_t *bytes, uint64_t nbytes, int start_bit, int width, int height,
+                    int n_stacks, uint8_t *raster, uint64_t *end_bit);
 
 #ifdef __cplusplus
 }

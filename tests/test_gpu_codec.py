@@ -50,3 +50,19 @@ def test_cli_depth4(pkg, plan4, tmp_path):
     q = plan4.encode_q(fr)
     dec = np.frombuffer(outf.read_bytes(), np.uint8).reshape(frames, h, w)
     assert np.array_equal(dec, plan4.decode_q(q, w, h, frames))
+
+
+@pytest.mark.parametrize("host_eg", ["0", "1"])
+def test_cli_decode_truncated_input_fails_cleanly(pkg, tmp_path, host_eg):
+    w, h, frames = 64, 48, 16
+    fr = pkg.synthetic.frames(w, h, frames, kind="uniform")
+    raw, binf, outf = tmp_path / "in.raw", tmp_path / "o.bin", tmp_path / "o.raw"
+    raw.write_bytes(fr.tobytes())
+    env = dict(os.environ, DCT3D_CODEC_HOST_EG=host_eg)
+    assert subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), "1"],
+                          capture_output=True, env=env).returncode == 0
+    data = binf.read_bytes()
+    binf.write_bytes(data[: len(data) // 2])
+    r = subprocess.run([pkg.CLI_PATH, "decode", str(binf), str(outf), str(w), str(h), str(frames), "1"],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 1 and "Truncated or corrupt" in r.stdout

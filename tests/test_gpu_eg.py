@@ -110,3 +110,72 @@ def test_encode_eg_batches_chain_like_one_stream(pkg, oracle, plan8, plan4, dept
         q = (plan8 if depth == 8 else plan4).encode_q(fr)
         exp, ebits = _expected(oracle, pkg, q, depth)
         assert tb_whole == ebits and whole == exp
+
+
+# ------------------------------------------------------------------------------------------------
+# decode (expGolomb_readValue / ExpGolombReader.java; Decoder.java:78-96 diagonal placement)
+# ------------------------------------------------------------------------------------------------
+def _dev_bytes(data: bytes):
+    import torch
+    pad = (-len(data)) % 4 + 8
+    return torch.from_numpy(np.frombuffer(data + bytes(pad), np.uint8).copy()).cuda()
+
+
+def _eg_decode(ctx, data: bytes, n_cubes: int, start_bit: int = 0):
+    import torch
+    dq = torch.zeros(n_cubes * ctx.cube_size, dtype=torch.int32, device="cuda")
+    eb = ctx.eg_decode_dev(_dev_bytes(data), len(data), start_bit, n_cubes, dq)
+    return dq.cpu().numpy().reshape(n_cubes, ctx.bd, 8, 8), eb
+
+
+@pytest.mark.parametrize("depth,kind", [(8, "ramp"), (8, "uniform"), (4, "ramp")])
+def test_eg_decode_round_trip_1080p(pkg, oracle, gpu_ctx8, gpu_ctx4, depth, kind):
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    q = ctx.encode_stacks(_frames(pkg, 1920, 1080, depth, kind))
+    data, nbits = _expected(oracle, pkg, q, depth)          # the oracle's (Java writer's) bytes
+    got, eb = _eg_decode(ctx, data, q.shape[0])
+    assert eb == nbits and np.array_equal(got, q)
+
+
+@pytest.mark.parametrize("n_cubes", [1, 5, 3000])
+def test_eg_decode_large_values_and_start_bits(pkg, oracle, gpu_ctx8, n_cubes):
+    rng = np.random.default_rng(7 + n_cubes)
+    q = rng.integers(-60, 61, size=(n_cubes, 8, 8, 8)).astype(np.int32)
+    q[rng.random(q.shape) < 0.5] = 0
+    big = rng.random(q.shape) < 0.01
+    q[big] = rng.integers(-(2**30) + 1, 2**30, size=int(big.sum()))      # long codes (up to 61 bits)
+    for start_bit in (0, 3, 7):
+        data, nbits = _expected(oracle, pkg, q, 8, 0x5A, start_bit)
+        got, eb = _eg_decode(gpu_ctx8, data + bytes(9), n_cubes, start_bit)  # trailing bytes are ignored
+        assert eb == nbits and np.array_equal(got, q), start_bit
+
+
+def test_eg_decode_truncated_and_corrupt(pkg, oracle, gpu_ctx8):
+    rng = np.random.default_rng(12)
+    q = rng.integers(-20, 21, size=(40, 8, 8, 8)).astype(np.int32)
+    data, nbits = _expected(oracle, pkg, q, 8)
+    with pytest.raises(pkg.Dct3dError) as e:
+        _eg_decode(gpu_ctx8, data[: len(data) // 2], 40)
+    assert e.value.code == pkg.DCT3D_ENODATA
+    got, eb = _eg_decode(gpu_ctx8, data[: len(data) // 2], 15)          # what is there decodes
+    assert np.array_equal(got, q[:15])
+    bad = bytearray(data)
+    bad[len(bad) // 3: len(bad) // 3 + 6] = bytes(6)                    # 48 zero bits: no valid code
+    with pytest.raises(pkg.Dct3dError) as e:
+        _eg_decode(gpu_ctx8, bytes(bad), 40)
+    assert e.value.code in (pkg.DCT3D_EINVAL, pkg.DCT3D_ENODATA)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_decode_eg_host_path_and_batches(pkg, oracle, plan8, plan4, depth):
+    """Host stream -> device entropy decode + dequantise + IDCT, in two batches continuing at the end
+    bit of the first: the frames equal the Java-semantics decode of the encoder's coefficients."""
+    plan = plan8 if depth == 8 else plan4
+    with pkg.Context(0, 8, 8, depth) as ctx:
+        fr = _frames(pkg, 64, 48, depth * 5, "uniform")
+        stream, tb = ctx.encode_eg(fr)
+        a, ea = ctx.decode_eg(stream, 64, 48, 2)
+        b, eb = ctx.decode_eg(stream[ea // 8:], 64, 48, 3, start_bit=ea % 8)
+        assert ea // 8 * 8 + eb == tb
+        q = plan.encode_q(fr)
+        assert np.array_equal(np.concatenate([a, b]), plan.decode_q(q, 64, 48, depth * 5))

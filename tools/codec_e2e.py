@@ -1,6 +1,6 @@
 """End-to-end codec timing (run on the GPU box): the reference-compatible CLI on a synthetic 1080p raw
 file, Exp-Golomb on the host (the reference's split: quantised ints over PCIe) vs on the device (only
-the stream crosses PCIe); both must write the same .bin.  Prints one JSON line."""
+the stream crosses PCIe), encode and decode; both must write the same .bin / frames.  One JSON line."""
 import importlib, json, os, subprocess, sys, tempfile, time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,12 +28,19 @@ for mode in ("1", "0"):
     res["encode_host_eg_s" if mode == "1" else "encode_device_eg_s"] = dt
 res["bin_identical"] = bins["0"] == bins["1"]
 res["bin_MB"] = len(bins["0"]) / 1e6
-t0 = time.perf_counter()
-r = subprocess.run([pkg.CLI_PATH, "decode", os.path.join(tmp, "out0.bin"), os.path.join(tmp, "dec.raw"), str(W), str(H),
-                    str(F), "1"], capture_output=True, text=True)
-res["decode_s"] = time.perf_counter() - t0
-assert r.returncode == 0, r.stdout + r.stderr
+decs = {}
+for mode in ("1", "0"):
+    env = dict(os.environ, DCT3D_CODEC_HOST_EG=mode)
+    dec = os.path.join(tmp, f"dec{mode}.raw")
+    t0 = time.perf_counter()
+    r = subprocess.run([pkg.CLI_PATH, "decode", os.path.join(tmp, "out0.bin"), dec, str(W), str(H), str(F), "1"],
+                       capture_output=True, text=True, env=env)
+    res["decode_host_eg_s" if mode == "1" else "decode_s"] = time.perf_counter() - t0
+    assert r.returncode == 0, r.stdout + r.stderr
+    decs[mode] = open(dec, "rb").read()
+res["decoded_identical"] = decs["0"] == decs["1"]
 res["encode_device_eg_fps"] = F / res["encode_device_eg_s"]
 res["encode_host_eg_fps"] = F / res["encode_host_eg_s"]
 res["decode_fps"] = F / res["decode_s"]
+res["decode_host_eg_fps"] = F / res["decode_host_eg_s"]
 print(json.dumps(res))
