@@ -1172,12 +1172,20 @@ int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, un
 // DCT3D_ENC_VARIANT (test/bench knob) selects one; default kDefaultVariant.
 namespace {
 constexpr int kDefaultVariant = 1;
+// Occupancy knob (DCT3D_LDS_PAD_KB, default from the occupancy sweep): extra dynamic LDS per block
+// limits the blocks per CU.  HBM3E serves the encode's 1:4 read/write stream faster from fewer
+// concurrent waves (tools/hbm_probe.hip: 5.68 TB/s at 8 waves/CU against 5.36 at 32).
+static size_t lds_pad(const char* var, int dflt_kb) {
+    const char* e = getenv(var);
+    return (size_t)(e ? atoi(e) : dflt_kb) * 1024;
+}
 template <int D, int ITER, bool NT, bool NTL = false>
 void launch_enc_t(const EncodeParams& P, hipStream_t st) {
+    static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t waves = (groups + ITER - 1) / ITER;
     const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode_kernel<D, ITER, NT, NTL>), dim3(blocks), dim3(kBlock), 0, st, P);
+    hipLaunchKernelGGL((encode_kernel<D, ITER, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
 }
 template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
@@ -1213,8 +1221,9 @@ int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st) {
 
 template <int PG>
 static void launch_dec_t(int D, uint32_t groups, const DecodeParams& P, hipStream_t st) {
-    if (D == 8) hipLaunchKernelGGL((decode_kernel<8, PG>), dim3(groups), dim3(kBlock), 0, st, P);
-    else hipLaunchKernelGGL((decode_kernel<4, PG>), dim3(groups), dim3(kBlock), 0, st, P);
+    static const size_t pad = lds_pad("DCT3D_DEC_LDS_PAD_KB", 0);
+    if (D == 8) hipLaunchKernelGGL((decode_kernel<8, PG>), dim3(groups), dim3(kBlock), pad, st, P);
+    else hipLaunchKernelGGL((decode_kernel<4, PG>), dim3(groups), dim3(kBlock), pad, st, P);
 }
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
