@@ -220,3 +220,89 @@ def test_read_cubes_quantisation_host_vs_reference(pkg, oracle, plan8, tmp_path)
         libc.fclose(f)
         files.append(path.read_bytes())
     assert files[0] == files[1]
+
+
+# ------------------------------------------------------------------------------------------------
+# entry points the device entropy stage uses (CPU: streams built by the oracle's Java writer)
+# ------------------------------------------------------------------------------------------------
+def _codec_stream_api(pkg):
+    L = codec(pkg)
+    L.dct3d_entropy_enc_create.restype = C.c_void_p
+    L.dct3d_entropy_enc_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p]
+    L.dct3d_entropy_enc_carry.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_int)]
+    L.dct3d_entropy_enc_push_stream.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
+    L.dct3d_entropy_enc_memory.restype = C.c_void_p
+    L.dct3d_entropy_enc_memory.argtypes = [C.c_void_p, C.POINTER(C.c_size_t)]
+    L.dct3d_entropy_enc_destroy.argtypes = [C.c_void_p]
+    L.dct3d_entropy_dec_create.restype = C.c_void_p
+    L.dct3d_entropy_dec_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_size_t]
+    L.dct3d_entropy_dec_window.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                           C.POINTER(C.c_int)]
+    L.dct3d_entropy_dec_consume.argtypes = [C.c_void_p, C.c_uint64]
+    L.dct3d_entropy_dec_destroy.argtypes = [C.c_void_p]
+    return L
+
+
+def _stream_bits(oracle, pkg, q, depth):
+    """the whole Exp-Golomb stream as a bit array, and the stream bit where each stack ends"""
+    cs = 64 * depth
+    pos = oracle.diagonal_slices(8, 8, depth)
+    vals = q.reshape(-1, cs)[:, pos[:, 0] + 8 * pos[:, 1] + 64 * pos[:, 2]]
+    v = vals.astype(np.int64)
+    code = np.where(v <= 0, -2 * v, 2 * v - 1) + 1
+    width = 2 * (np.floor(np.log2(code.astype(np.float64))).astype(np.int64) + 1) - 1
+    nbits = int(width.sum())
+    bits = np.unpackbits(np.frombuffer(oracle.eg_write(vals.ravel().astype(np.int32)), np.uint8))[:nbits]
+    return bits, width
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3])
+def test_push_stream_equals_per_stack_entropy(pkg, oracle, plan8, batch):
+    """dct3d_entropy_enc_push_stream (a stream built elsewhere, continuing the carried partial byte,
+    one deflate call per batch) writes the same .bin as the per-stack host path."""
+    w, h, stacks = 48, 32, 5
+    fr = pkg.synthetic.frames(w, h, stacks * 8, kind="uniform")
+    q = plan8.encode_q(fr)
+    bits, width = _stream_bits(oracle, pkg, q, 8)
+    per_stack = width.reshape(stacks, -1).sum(1)
+    ends = np.cumsum(per_stack)
+    L = _codec_stream_api(pkg)
+    e = L.dct3d_entropy_enc_create(w, h, 8, None)
+    start = 0
+    for s0 in range(0, stacks, batch):
+        s1 = min(stacks, s0 + batch)
+        end = int(ends[s1 - 1])
+        cb, cbits = C.c_uint8(), C.c_int()
+        L.dct3d_entropy_enc_carry(e, C.byref(cb), C.byref(cbits))
+        byte0 = start // 8
+        assert cbits.value == start % 8
+        chunk = np.packbits(bits[byte0 * 8:end]).tobytes()
+        if cbits.value:
+            assert chunk[0] >> (8 - cbits.value) == cb.value >> (8 - cbits.value)
+        assert L.dct3d_entropy_enc_push_stream(e, chunk, end - byte0 * 8, int(s1 == stacks)) == 0
+        start = end
+    n = C.c_size_t()
+    got = C.string_at(L.dct3d_entropy_enc_memory(e, C.byref(n)), n.value)
+    L.dct3d_entropy_enc_destroy(e)
+    assert got == entropy_encode(pkg, q, w, h, stacks, 8)
+
+
+def test_decoder_window_and_consume(pkg, plan8):
+    """dct3d_entropy_dec_window exposes the inflated stream from the current bit; consume advances it."""
+    w, h, stacks = 48, 32, 3
+    q = plan8.encode_q(pkg.synthetic.frames(w, h, stacks * 8, kind="ramp"))
+    b = entropy_encode(pkg, q, w, h, stacks, 8)
+    raw = zlib.decompress(b)
+    L = _codec_stream_api(pkg)
+    buf = C.create_string_buffer(b, len(b))
+    d = L.dct3d_entropy_dec_create(w, h, 8, None, buf, len(b))
+    p, n, bit = C.c_void_p(), C.c_size_t(), C.c_int()
+    assert L.dct3d_entropy_dec_window(d, 1 << 20, C.byref(p), C.byref(n), C.byref(bit)) == 0
+    assert bit.value == 0 and C.string_at(p, n.value) == raw           # whole stream available
+    L.dct3d_entropy_dec_consume(d, 8 * 5 + 3)
+    assert L.dct3d_entropy_dec_window(d, 16, C.byref(p), C.byref(n), C.byref(bit)) == 0
+    assert bit.value == 3 and C.string_at(p, n.value) == raw[5:]
+    L.dct3d_entropy_dec_consume(d, 3 + 8 * 2 + 6)                      # from the window's first byte
+    assert L.dct3d_entropy_dec_window(d, 16, C.byref(p), C.byref(n), C.byref(bit)) == 0
+    assert bit.value == 1 and C.string_at(p, n.value) == raw[8:]
+    L.dct3d_entropy_dec_destroy(d)
