@@ -12,7 +12,8 @@ constexpr int kMaxGroupsDev = 64;  // == kMaxGroups in dct3d_plan.h; one LDS slo
 struct EncodeParams {
     const uint8_t* raster;
     int32_t* out;
-    uint32_t n_cubes;          // cubes in this launch (whole stacks)
+    uint32_t n_cubes;          // end of this launch's cube range (global index, whole stacks)
+    uint32_t g_base;           // first cube of this launch (global index; 0 unless a tail launch)
     uint32_t cubes_per_stack;
     uint32_t nbx;              // cubes per block-row
     uint32_t width;

@@ -263,11 +263,12 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
     const int so = kz + kx0;
 
     uint2 rawn[D];
-    load_rows<D, NTL>(P, group0 * kCubesPerWave + c, group0 * kCubesPerWave + c < P.n_cubes, j, rawn);
+    load_rows<D, NTL>(P, P.g_base + group0 * kCubesPerWave + c, P.g_base + group0 * kCubesPerWave + c < P.n_cubes, j,
+                      rawn);
 
 #pragma unroll 1
     for (int it = 0; it < ITER; it++) {
-        const uint32_t cube0 = (group0 + it) * kCubesPerWave;
+        const uint32_t cube0 = P.g_base + (group0 + it) * kCubesPerWave;
         if (cube0 >= P.n_cubes) break;  // wave-uniform
         const uint32_t g = cube0 + c;
         const bool valid = g < P.n_cubes;
@@ -301,22 +302,38 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
             rr[i] = P.tab_rstep[sz + i];
             thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
         }
+        // Uncertified coefficients: 8x8x4 (INL) appends them to the flag list inside the row loop while
+        // q is in registers -- its exact ties (the 4-point k = 2 row is +-1/2) flag a quarter of the
+        // waves; 8x8x8 (flags in ~5 % of waves, registers at the 128 limit) re-derives them after the
+        // stores from reloaded rows instead.
+        constexpr bool INL = (D == 4);
         int32_t qv[8][NB];
-        int flag = 0;
+        int overflow = 0, flag = 0;
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) {
             pin(b[ky]);
             bool f = false;
+            float qq[NB];
 #pragma unroll
             for (int x = 0; x < NB; x++) {
-                const float q = b[ky][x] * rr[ky + x];
-                const float n = __builtin_rintf(q);
-                f |= __builtin_fabsf(q - n) >= thr[ky + x];
+                qq[x] = b[ky][x] * rr[ky + x];
+                const float n = __builtin_rintf(qq[x]);
+                f |= __builtin_fabsf(qq[x] - n) >= thr[ky + x];
                 qv[ky][x] = (int32_t)n;
             }
-            flag |= (int)f;
+            if (!INL) flag |= (int)f;
+            if (INL && __builtin_expect(f && valid, 0)) {
+#pragma unroll
+                for (int x = 0; x < NB; x++)
+                    if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) {
+                        const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
+                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
+                        else overflow = 1;
+                    }
+            }
             pin(qv[ky]);
-            asm volatile("" : "+v"(flag));  // the row's checks complete here (q, n die)
+            asm volatile("" : "+v"(overflow), "+v"(flag));  // the row's checks complete here (q, n die)
         }
         if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
 
@@ -358,15 +375,14 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
             wave_lds_sync();
         }
 
-        // ---- rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
-        if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
+        // ---- !INL rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
+        if (!INL && __builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
             uint2 raw2[D];
             load_rows<D>(P, g, valid, j, raw2);
             float a2[D][8];
             to_float<D>(raw2, a2);
             float b2[8][NB];
             forward_cube<D, NB>(a2, m, c, j, wl, b2);
-            bool overflow = false;
             if (flag && valid) {
 #pragma unroll
                 for (int ky = 0; ky < 8; ky++)
@@ -379,18 +395,20 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
                             const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
                             const uint32_t idx = atomicAdd(&P.counters[0], 1u);
                             if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
-                            else overflow = true;
+                            else overflow = 1;
                         }
                     }
             }
-            // at most one cube-list entry per cube: the lowest overflowing lane of the cube appends
-            const unsigned long long ov = __ballot(overflow);
+            wave_lds_sync();
+        }
+        // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
+        const unsigned long long ov = __ballot(overflow != 0);
+        if (__builtin_expect(ov != 0ull, 0)) {
             const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
             if (overflow && (__builtin_ctz(mine) == j)) {
                 const uint32_t idx = atomicAdd(&P.counters[1], 1u);
                 P.cube_list[idx] = g;  // capacity n_cubes: never overflows
             }
-            wave_lds_sync();
         }
     }
 }
@@ -1182,7 +1200,7 @@ static size_t lds_pad(const char* var, int dflt_kb) {
 template <int D, int ITER, bool NT, bool NTL = false>
 void launch_enc_t(const EncodeParams& P, hipStream_t st) {
     static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);
-    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
+    const uint32_t groups = (P.n_cubes - P.g_base + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t waves = (groups + ITER - 1) / ITER;
     const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL((encode_kernel<D, ITER, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);

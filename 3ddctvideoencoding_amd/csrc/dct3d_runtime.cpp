@@ -338,6 +338,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.raster = d_raster;
     P.out = d_q;
     P.n_cubes = (uint32_t)n_cubes;
+    P.g_base = 0;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
     P.width = (uint32_t)w;
