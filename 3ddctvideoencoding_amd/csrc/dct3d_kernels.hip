@@ -244,10 +244,10 @@ __device__ __forceinline__ void store16(void* p, const int4& v) {
     }
 }
 
-// One wave = ITER consecutive groups of 8 cubes; the rows of group it+1 are loaded (16 VGPRs)
-// before group it is transformed, so every wave keeps loads in flight while it computes.
-template <int D, int ITER, bool NT, bool NTL = false>
-__global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(EncodeParams P) {
+// One wave = one group of 8 consecutive cubes (register-prefetch loops over several groups spill
+// and were 25-40 % slower: profiles/r01/encode_variant_sweep.txt).
+template <int D, bool NT, bool NTL = false>
+__global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
     constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
@@ -256,29 +256,17 @@ __global__ __launch_bounds__(kBlock, ITER == 1 ? 4 : 3) void encode_kernel(Encod
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = lane >> 3, j = lane & 7;
     char* wl = lds + wave * kWaveLds;
-    const uint32_t group0 = (blockIdx.x * kWavesPerBlock + wave) * ITER;
 
     const int kz = (D == 8) ? j : (j >> 1);
     const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
     const int so = kz + kx0;
 
-    uint2 rawn[D];
-    load_rows<D, NTL>(P, P.g_base + group0 * kCubesPerWave + c, P.g_base + group0 * kCubesPerWave + c < P.n_cubes, j,
-                      rawn);
-
-#pragma unroll 1
-    for (int it = 0; it < ITER; it++) {
-        const uint32_t cube0 = P.g_base + (group0 + it) * kCubesPerWave;
-        if (cube0 >= P.n_cubes) break;  // wave-uniform
+    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
+    uint2 raw[D];
+    load_rows<D, NTL>(P, cube0 + c, cube0 + c < P.n_cubes, j, raw);  // in flight before anything else
+    if (cube0 < P.n_cubes) {  // wave-uniform
         const uint32_t g = cube0 + c;
         const bool valid = g < P.n_cubes;
-        uint2 raw[D];
-#pragma unroll
-        for (int z = 0; z < D; z++) raw[z] = rawn[z];
-        if (it + 1 < ITER) {
-            const uint32_t gn = cube0 + kCubesPerWave + c;
-            load_rows<D, NTL>(P, gn, gn < P.n_cubes, j, rawn);  // prefetch the next group
-        }
 
         float a[D][8];
         to_float<D>(raw, a);
@@ -485,172 +473,6 @@ __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
 // =============================================================================================
 // Fused decode (fp64, certified)
 // =============================================================================================
-template <int D>
-__global__ __launch_bounds__(kBlock) void decode_kernel_v0(DecodeParams P) {
-    constexpr int CS = 64 * D;
-    constexpr int NB = (D == 8) ? 8 : 4;
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int c = lane >> 3, j = lane & 7;
-    char* wl = lds + wave * kWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
-    const uint32_t g = cube0 + c;
-    const bool valid = g < P.n_cubes;
-    const int kz = (D == 8) ? j : (j >> 1);
-    const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
-
-    // ---- staged loads: 8 KiB rounds, 1 KiB per instruction, into the face-padded layout ----
-    constexpr int ROUNDS = (D == 8) ? 2 : 1;
-    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
-    double b[8][NB];
-    double amax = 0.0;
-#pragma unroll
-    for (int rd = 0; rd < ROUNDS; rd++) {
-        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
-        const char* inb = (const char*)(P.in + (size_t)rcube0 * CS);
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int q = t * 64 + lane;
-            const int cc = q / (CS / 4);
-            const int face = (q >> 4) % D;
-            const int w = q & 15;
-            int4 v = make_int4(0, 0, 0, 0);
-            if (rcube0 + cc < P.n_cubes) v = *(const int4*)(inb + (size_t)q * 16);
-            *(int4*)(wl + (cc * D + face) * kFace + w * 16) = v;
-        }
-        wave_lds_sync();
-        if ((c / CUBES_PER_ROUND) == rd) {
-            const int cc = c % CUBES_PER_ROUND;
-#pragma unroll
-            for (int ky = 0; ky < 8; ky++) {
-                if constexpr (D == 8) {
-#pragma unroll
-                    for (int h = 0; h < 2; h++) {
-                        const int4 v = *(const int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16);
-                        const int vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (int e = 0; e < 4; e++) {
-                            const int kx = 4 * h + e;
-                            const double cf = (double)vv[e] * (double)max(1, 5 * (kx + ky + kz));
-                            b[ky][4 * h + e] = cf;
-                            amax = fmax(amax, fabs(cf));
-                        }
-                    }
-                } else {
-                    const int4 v = *(const int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16);
-                    const int vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        const int kx = kx0 + e;
-                        const double cf = (double)vv[e] * (double)max(1, 5 * (kx + ky + kz));
-                        b[ky][e] = cf;
-                        amax = fmax(amax, fabs(cf));
-                    }
-                }
-            }
-        }
-        wave_lds_sync();
-    }
-#pragma unroll
-    for (int o = 1; o < 8; o <<= 1) amax = fmax(amax, __shfl_xor(amax, o, 64));
-
-    // ---- inverse pass Y (face layout) ----
-#pragma unroll
-    for (int x = 0; x < NB; x++) {
-        double col[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = b[y][x];
-        idct8(col);
-#pragma unroll
-        for (int y = 0; y < 8; y++) b[y][x] = col[y];
-    }
-
-    // ---- LDS transpose in 4 quarter rounds (kx pairs): face layout -> row layout (c, y)[kz][kx] ----
-    double a[D][8];
-#pragma unroll
-    for (int qr = 0; qr < 4; qr++) {
-        const bool writer = (D == 8) || ((j & 1) == (qr >> 1));
-        if (writer) {
-            const int xl = (D == 8) ? 2 * qr : 2 * (qr & 1);  // local kx index inside b
-#pragma unroll
-            for (int y = 0; y < 8; y++)
-                *(double2*)(wl + (c * 8 + y) * kSlot + kz * 16) = make_double2(b[y][xl], b[y][xl + 1]);
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int z = 0; z < D; z++) {
-            const double2 t = *(const double2*)(wl + (c * 8 + j) * kSlot + z * 16);
-            a[z][2 * qr] = t.x;
-            a[z][2 * qr + 1] = t.y;
-        }
-        wave_lds_sync();
-    }
-
-    // ---- inverse pass X, inverse pass Z (row layout, y = j) ----
-#pragma unroll
-    for (int z = 0; z < D; z++) idct8(a[z]);
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-        double col[D];
-#pragma unroll
-        for (int z = 0; z < D; z++) col[z] = a[z][x];
-        idctN<D>(col);
-#pragma unroll
-        for (int z = 0; z < D; z++) a[z][x] = col[z];
-    }
-
-    // ---- certify, clamp + truncate (InverseDCT.java:74-80, Decoder.java:112), store rows ----
-    const double margin = amax * P.dec_G + P.dec_E;
-    bool flag = false;
-    uint2 outw[D];
-#pragma unroll
-    for (int z = 0; z < D; z++) {
-        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-        for (int x = 0; x < 8; x++) {
-            const double v = a[z][x];
-            const double r = rint(v);
-            flag |= (r >= 1.0) & (r <= 255.0) & (fabs(v - r) <= margin);
-            const uint32_t px = v <= 0.0 ? 0u : (v >= 255.0 ? 255u : (uint32_t)v);
-            if (x < 4) w0 |= px << (8 * x);
-            else w1 |= px << (8 * (x - 4));
-        }
-        outw[z] = make_uint2(w0, w1);
-    }
-    if (valid) {
-        const uint32_t s = g / P.cubes_per_stack;
-        const uint32_t r = g - s * P.cubes_per_stack;
-        const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
-        uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + j) * P.width + bx * 8;
-#pragma unroll
-        for (int z = 0; z < D; z++) *(uint2*)(dst + (size_t)z * P.plane) = outw[z];
-    }
-    if (__builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
-        bool overflow = false;
-        if (flag && valid) {
-#pragma unroll
-            for (int z = 0; z < D; z++)
-#pragma unroll
-                for (int x = 0; x < 8; x++) {
-                    const double v = a[z][x];
-                    const double r = rint(v);
-                    if ((r >= 1.0) & (r <= 255.0) & (fabs(v - r) <= margin)) {
-                        const uint32_t n = (uint32_t)((z * 8 + j) * 8 + x);
-                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + n;
-                        else overflow = true;
-                    }
-                }
-        }
-        const unsigned long long ov = __ballot(overflow);
-        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
-        if (overflow && (__builtin_ctz(mine) == j)) {
-            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-            P.cube_list[idx] = g;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------------
 // Decode v1: 2*D lanes per cube, 32 doubles per lane (<= 128 VGPRs, 4 waves per SIMD).
 //   lane = c2*32 + h*16 + c1*D + k   (cube c = c2*(CPW/2) + c1; h = bit 4; k = low bits)
@@ -1185,36 +1007,31 @@ int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, un
 // =============================================================================================
 // Launchers
 // =============================================================================================
-// Encode variants (template <D, ITER, NT>): ITER = 8-cube groups per wave (register prefetch
-// pipeline depth along the wave's cubes), NT = non-temporal stores of the int32 output.
-// DCT3D_ENC_VARIANT (test/bench knob) selects one; default kDefaultVariant.
+// Encode variants (DCT3D_ENC_VARIANT, test/bench knob): 0 plain stores, 1 non-temporal stores of the
+// int32 output (default), 2 non-temporal stores and loads (profiles/r01/encode_variant_sweep.txt).
 namespace {
 constexpr int kDefaultVariant = 1;
-// Occupancy knob (DCT3D_LDS_PAD_KB, default from the occupancy sweep): extra dynamic LDS per block
-// limits the blocks per CU.  HBM3E serves the encode's 1:4 read/write stream faster from fewer
-// concurrent waves (tools/hbm_probe.hip: 5.68 TB/s at 8 waves/CU against 5.36 at 32).
+// Occupancy knob (DCT3D_*_LDS_PAD_KB): extra dynamic LDS per block limits the blocks per CU.  HBM3E
+// serves the encode's 1:4 read/write stream faster from fewer concurrent waves (tools/hbm_probe.hip:
+// 5.68 TB/s at 8 waves/CU against 5.36 at 32), but both kernels need the occupancy to hide their own
+// latency (tools/occupancy_sweep.sh), so the default pad is 0.
 static size_t lds_pad(const char* var, int dflt_kb) {
     const char* e = getenv(var);
     return (size_t)(e ? atoi(e) : dflt_kb) * 1024;
 }
-template <int D, int ITER, bool NT, bool NTL = false>
+template <int D, bool NT, bool NTL = false>
 void launch_enc_t(const EncodeParams& P, hipStream_t st) {
     static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);
     const uint32_t groups = (P.n_cubes - P.g_base + kCubesPerWave - 1) / kCubesPerWave;
-    const uint32_t waves = (groups + ITER - 1) / ITER;
-    const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode_kernel<D, ITER, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
+    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((encode_kernel<D, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
 }
 template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
     switch (v) {
-        case 0: launch_enc_t<D, 1, false>(P, st); break;
-        case 1: launch_enc_t<D, 1, true>(P, st); break;
-        case 2: launch_enc_t<D, 4, false>(P, st); break;
-        case 3: launch_enc_t<D, 4, true>(P, st); break;
-        case 4: launch_enc_t<D, 16, false>(P, st); break;
-        case 5: launch_enc_t<D, 16, true>(P, st); break;
-        default: launch_enc_t<D, 1, true, true>(P, st); break;  // 6: NT stores + NT loads
+        case 0: launch_enc_t<D, false>(P, st); break;
+        case 2: launch_enc_t<D, true, true>(P, st); break;
+        default: launch_enc_t<D, true>(P, st); break;
     }
 }
 }  // namespace
@@ -1248,27 +1065,19 @@ int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     static int variant = -1;
     if (variant < 0) {
-        const char* e = getenv("DCT3D_DEC_VARIANT");  // 0: 8 lanes per cube (previous kernel)
+        const char* e = getenv("DCT3D_DEC_VARIANT");
         variant = e ? atoi(e) : 1;
     }
-    if (variant == 0) {
-        const uint32_t per = kCubesPerWave * kWavesPerBlock;
-        const uint32_t groups = (uint32_t)((P.n_cubes + per - 1) / per);
-        if (D == 8) hipLaunchKernelGGL(decode_kernel_v0<8>, dim3(groups), dim3(kBlock), 0, st, P);
-        else hipLaunchKernelGGL(decode_kernel_v0<4>, dim3(groups), dim3(kBlock), 0, st, P);
-    } else {
-        const uint32_t per = (D == 8 ? DecGeom<8>::CPW : DecGeom<4>::CPW) * kWavesPerBlock;
-        const uint32_t groups = (uint32_t)((P.n_cubes + per - 1) / per);
-        // (non-temporal dword output stores were measured 26 % slower: 3.18 vs 2.51 ms, c3)
-        // 1: one butterfly per pin group (default); 4: unpinned (pin groups 1/2/4/none measured
-        // within 1 %); 7 / 8: diagnostics, memory-only / compute-only (output NOT valid)
-        switch (variant) {
-            case 4: launch_dec_t<0>(D, groups, P, st); break;
-            case 7: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, st, P); break;
-            case 8: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, st, P); break;
-
-            default: launch_dec_t<1>(D, groups, P, st); break;
-        }
+    const uint32_t per = (D == 8 ? DecGeom<8>::CPW : DecGeom<4>::CPW) * kWavesPerBlock;
+    const uint32_t groups = (uint32_t)((P.n_cubes + per - 1) / per);
+    // 1: one butterfly per pin group (default); 4: unpinned (pin groups 1/2/4/none measured within
+    // 1 %); 7 / 8: diagnostics, memory-only / compute-only (output NOT valid).  Non-temporal dword
+    // output stores were 26 % slower (profiles/r01/decode_variant_sweep.txt).
+    switch (variant) {
+        case 4: launch_dec_t<0>(D, groups, P, st); break;
+        case 7: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, st, P); break;
+        case 8: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, st, P); break;
+        default: launch_dec_t<1>(D, groups, P, st); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/sweep
 VE=${VAR_ENV:-DCT3D_ENC_VARIANT}
 K=${TESTS:-encode_64x64 or ragged or encode_1080p_stack or overflow or depth4}
 i=0
-for v in ${VARIANTS:-0 1 2 3 4 5}; do
+for v in ${VARIANTS:-0 1 2}; do
   i=$((i+1))
   env $VE=$v timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "$K" > gpurun_out/sweep/pytest_v$v.log 2>&1
   rc=$?; echo "variant $v pytest rc=$rc $(tail -1 gpurun_out/sweep/pytest_v$v.log)"
