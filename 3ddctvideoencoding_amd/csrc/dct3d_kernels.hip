@@ -244,161 +244,164 @@ __device__ __forceinline__ void store16(void* p, const int4& v) {
     }
 }
 
-// One wave = one group of 8 consecutive cubes (register-prefetch loops over several groups spill
-// and were 25-40 % slower: profiles/r01/encode_variant_sweep.txt).
-template <int D, bool NT, bool NTL = false>
-__global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
+// Everything after the row loads, for the 8 cubes from cube0: statistics, transform, quantise +
+// certify, staged 1 KiB stores, uncertified coefficients to the flag list.
+template <int D, bool NT>
+__device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (&raw)[D], char* wl, int lane,
+                                            uint32_t cube0) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
     constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
-
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c = lane >> 3, j = lane & 7;
-    char* wl = lds + wave * kWaveLds;
-
     const int kz = (D == 8) ? j : (j >> 1);
     const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
     const int so = kz + kx0;
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
 
-    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
-    uint2 raw[D];
-    load_rows<D, NTL>(P, cube0 + c, cube0 + c < P.n_cubes, j, raw);  // in flight before anything else
-    if (cube0 < P.n_cubes) {  // wave-uniform
-        const uint32_t g = cube0 + c;
-        const bool valid = g < P.n_cubes;
+    float a[D][8];
+    to_float<D>(raw, a);
+    uint32_t S;
+    int m;
+    float A;
+    cube_stats<D>(raw, a, S, m, A);
+    asm volatile("" : "+v"(S), "+v"(m), "+v"(A));  // stats now: raw dies after conversion
 
-        float a[D][8];
-        to_float<D>(raw, a);
-        uint32_t S;
-        int m;
-        float A;
-        cube_stats<D>(raw, a, S, m, A);
-        asm volatile("" : "+v"(S), "+v"(m), "+v"(A));  // stats now: raw dies after conversion
+    float b[8][NB];
+    forward_cube<D, NB>(a, m, c, j, wl, b);
 
-        float b[8][NB];
-        forward_cube<D, NB>(a, m, c, j, wl, b);
-
-        // ---- quantise + certify (thr_s = 0.5 - (A*G_s + E_s), dct3d_plan.cpp) ----
-        // The per-lane tables are re-read each iteration (an opaque zero keeps the compiler from
-        // hoisting ~45 loop-invariant registers out of the loop; the reads hit L1/L2).
-        int sz = so;
-        asm volatile("" : "+v"(sz));
-        float rr[NI], thr[NI];
+    // ---- quantise + certify (thr_s = 0.5 - (A*G_s + E_s), dct3d_plan.cpp) ----
+    // The per-lane tables are re-read each iteration (an opaque zero keeps the compiler from
+    // hoisting ~45 loop-invariant registers out of the loop; the reads hit L1/L2).
+    int sz = so;
+    asm volatile("" : "+v"(sz));
+    float rr[NI], thr[NI];
 #pragma unroll
-        for (int i = 0; i < NI; i++) {
-            rr[i] = P.tab_rstep[sz + i];
-            thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
+    for (int i = 0; i < NI; i++) {
+        rr[i] = P.tab_rstep[sz + i];
+        thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
+    }
+    // Uncertified coefficients: 8x8x4 (INL) appends them to the flag list inside the row loop while
+    // q is in registers -- its exact ties (the 4-point k = 2 row is +-1/2) flag a quarter of the
+    // waves; 8x8x8 (flags in ~5 % of waves, registers at the 128 limit) re-derives them after the
+    // stores from reloaded rows instead.
+    constexpr bool INL = (D == 4);
+    int32_t qv[8][NB];
+    int overflow = 0, flag = 0;
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++) {
+        pin(b[ky]);
+        bool f = false;
+        float qq[NB];
+#pragma unroll
+        for (int x = 0; x < NB; x++) {
+            qq[x] = b[ky][x] * rr[ky + x];
+            const float n = __builtin_rintf(qq[x]);
+            f |= __builtin_fabsf(qq[x] - n) >= thr[ky + x];
+            qv[ky][x] = (int32_t)n;
         }
-        // Uncertified coefficients: 8x8x4 (INL) appends them to the flag list inside the row loop while
-        // q is in registers -- its exact ties (the 4-point k = 2 row is +-1/2) flag a quarter of the
-        // waves; 8x8x8 (flags in ~5 % of waves, registers at the 128 limit) re-derives them after the
-        // stores from reloaded rows instead.
-        constexpr bool INL = (D == 4);
-        int32_t qv[8][NB];
-        int overflow = 0, flag = 0;
+        if (!INL) flag |= (int)f;
+        if (INL && __builtin_expect(f && valid, 0)) {
 #pragma unroll
-        for (int ky = 0; ky < 8; ky++) {
-            pin(b[ky]);
-            bool f = false;
-            float qq[NB];
+            for (int x = 0; x < NB; x++)
+                if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) {
+                    const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
+                    const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                    if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
+                    else overflow = 1;
+                }
+        }
+        pin(qv[ky]);
+        asm volatile("" : "+v"(overflow), "+v"(flag));  // the row's checks complete here (q, n die)
+    }
+    if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+
+    // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
+    constexpr int ROUNDS = (D == 8) ? 2 : 1;
+    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
 #pragma unroll
-            for (int x = 0; x < NB; x++) {
-                qq[x] = b[ky][x] * rr[ky + x];
-                const float n = __builtin_rintf(qq[x]);
-                f |= __builtin_fabsf(qq[x] - n) >= thr[ky + x];
-                qv[ky][x] = (int32_t)n;
+    for (int rd = 0; rd < ROUNDS; rd++) {
+        if ((c / CUBES_PER_ROUND) == rd) {
+            const int cc = c % CUBES_PER_ROUND;
+            if constexpr (D == 8) {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+                        *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
+                            make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
+            } else {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+                    *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
+                        make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
             }
-            if (!INL) flag |= (int)f;
-            if (INL && __builtin_expect(f && valid, 0)) {
+        }
+        wave_lds_sync();
+        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
+        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
 #pragma unroll
-                for (int x = 0; x < NB; x++)
-                    if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) {
+        for (int t = 0; t < 8; t++) {
+            const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
+            const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
+            const int face = (q >> 4) % D;
+            const int w = q & 15;
+            if (rcube0 + cc < P.n_cubes) {
+                const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
+                store16<NT>(outb + (size_t)q * 16, v);
+            }
+        }
+        wave_lds_sync();
+    }
+
+    // ---- !INL rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
+    if (!INL && __builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
+        uint2 raw2[D];
+        load_rows<D>(P, g, valid, j, raw2);
+        float a2[D][8];
+        to_float<D>(raw2, a2);
+        float b2[8][NB];
+        forward_cube<D, NB>(a2, m, c, j, wl, b2);
+        if (flag && valid) {
+#pragma unroll
+            for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                for (int x = 0; x < NB; x++) {
+                    const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
+                    const float q = b2[ky][x] * rr[ky + x];
+                    const float n = __builtin_rintf(q);
+                    if (__builtin_fabsf(q - n) >= th2) {
                         const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
                         const uint32_t idx = atomicAdd(&P.counters[0], 1u);
                         if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
                         else overflow = 1;
                     }
-            }
-            pin(qv[ky]);
-            asm volatile("" : "+v"(overflow), "+v"(flag));  // the row's checks complete here (q, n die)
-        }
-        if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
-
-        // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
-        constexpr int ROUNDS = (D == 8) ? 2 : 1;
-        constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
-#pragma unroll
-        for (int rd = 0; rd < ROUNDS; rd++) {
-            if ((c / CUBES_PER_ROUND) == rd) {
-                const int cc = c % CUBES_PER_ROUND;
-                if constexpr (D == 8) {
-#pragma unroll
-                    for (int ky = 0; ky < 8; ky++)
-#pragma unroll
-                        for (int h = 0; h < 2; h++)
-                            *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
-                                make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
-                } else {
-#pragma unroll
-                    for (int ky = 0; ky < 8; ky++)
-                        *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
-                            make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
                 }
-            }
-            wave_lds_sync();
-            const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
-            char* outb = (char*)(P.out + (size_t)rcube0 * CS);
-#pragma unroll
-            for (int t = 0; t < 8; t++) {
-                const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
-                const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
-                const int face = (q >> 4) % D;
-                const int w = q & 15;
-                if (rcube0 + cc < P.n_cubes) {
-                    const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
-                    store16<NT>(outb + (size_t)q * 16, v);
-                }
-            }
-            wave_lds_sync();
         }
-
-        // ---- !INL rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
-        if (!INL && __builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
-            uint2 raw2[D];
-            load_rows<D>(P, g, valid, j, raw2);
-            float a2[D][8];
-            to_float<D>(raw2, a2);
-            float b2[8][NB];
-            forward_cube<D, NB>(a2, m, c, j, wl, b2);
-            if (flag && valid) {
-#pragma unroll
-                for (int ky = 0; ky < 8; ky++)
-#pragma unroll
-                    for (int x = 0; x < NB; x++) {
-                        const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
-                        const float q = b2[ky][x] * rr[ky + x];
-                        const float n = __builtin_rintf(q);
-                        if (__builtin_fabsf(q - n) >= th2) {
-                            const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
-                            const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                            if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
-                            else overflow = 1;
-                        }
-                    }
-            }
-            wave_lds_sync();
-        }
-        // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
-        const unsigned long long ov = __ballot(overflow != 0);
-        if (__builtin_expect(ov != 0ull, 0)) {
-            const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
-            if (overflow && (__builtin_ctz(mine) == j)) {
-                const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-                P.cube_list[idx] = g;  // capacity n_cubes: never overflows
-            }
+        wave_lds_sync();
+    }
+    // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
+    const unsigned long long ov = __ballot(overflow != 0);
+    if (__builtin_expect(ov != 0ull, 0)) {
+        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
+        if (overflow && (__builtin_ctz(mine) == j)) {
+            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
         }
     }
+
+}
+
+// One wave = one group of 8 consecutive cubes (register-prefetch loops over several groups spill
+// and were 25-40 % slower: profiles/r01/encode_variant_sweep.txt).
+template <int D, bool NT, bool NTL = false>
+__global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
+    uint2 raw[D];
+    load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
+    if (cube0 < P.n_cubes) encode_body<D, NT>(P, raw, lds + wave * kWaveLds, lane, cube0);  // wave-uniform
 }
 
 // =============================================================================================
