@@ -37,7 +37,7 @@ ABI_SYMBOLS = (
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
     "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev",
     "dct3d_eg_encode_dev", "dct3d_encode_eg", "dct3d_eg_fetch", "dct3d_diagonal_order",
-    "dct3d_eg_decode_dev", "dct3d_decode_eg",
+    "dct3d_eg_decode_dev", "dct3d_decode_eg", "dct3d_encode_eg_dev",
 )
 
 
@@ -101,6 +101,7 @@ def lib() -> C.CDLL:
         L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
         L.dct3d_eg_encode_dev.argtypes = [vp, vp, u64, C.c_uint8, i32, vp, u64, C.POINTER(u64)]
         L.dct3d_encode_eg.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, C.POINTER(u64)]
+        L.dct3d_encode_eg_dev.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, vp, u64, C.POINTER(u64)]
         L.dct3d_eg_fetch.argtypes = [vp, vp, u64]
         L.dct3d_diagonal_order.argtypes = [i32, i32, i32, vp]
         L.dct3d_eg_decode_dev.argtypes = [vp, vp, u64, u64, u64, vp, C.POINTER(u64)]
@@ -281,6 +282,16 @@ class Context:
         tb = C.c_uint64(0)
         _check(lib().dct3d_eg_encode_dev(self._h, _tptr(d_q), n_cubes, carry_byte, carry_bits, _tptr(d_out), out_cap,
                                          C.byref(tb)), "dct3d_eg_encode_dev")
+        return tb.value
+
+    def encode_eg_dev(self, d_frames, width: int, height: int, n_stacks: int, d_out, out_cap: int,
+                      carry_byte: int = 0, carry_bits: int = 0) -> int:
+        """Fused device path: u8 frames (device) -> Exp-Golomb stream words in d_out, no int32
+        intermediate; returns the total bits (carry included).  Dct3dError(DCT3D_ENOSPC) if out_cap is
+        too small."""
+        tb = C.c_uint64(0)
+        _check(lib().dct3d_encode_eg_dev(self._h, _tptr(d_frames), width, height, n_stacks, carry_byte, carry_bits,
+                                         _tptr(d_out), out_cap, C.byref(tb)), "dct3d_encode_eg_dev")
         return tb.value
 
     def encode_eg(self, frames: np.ndarray, carry_byte: int = 0, carry_bits: int = 0) -> tuple[bytes, int]:

@@ -255,6 +255,59 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
     if (g + 1 == P.n_cubes || (end >> 5) != wl) P.out[wl] = P.tail[g];
 }
 
+// Fused path, K3: one wave per segment (8 cubes, coded by encode_eg_kernel into lane-interleaved
+// slot words).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are shifted
+// into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane has
+// >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
+// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.
+__global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
+                                                              const uint16_t* __restrict__ lane_bits, uint32_t lcap) {
+    if (P.status[1] != 0) return;  // capacity failure: nothing is written
+    const int lane = threadIdx.x & 63;
+    const uint64_t s = (uint64_t)blockIdx.x * kEgWaves + (threadIdx.x >> 6);
+    if (s >= P.n_cubes) return;
+    const uint32_t lb = lane_bits[s * 64 + lane];
+    uint32_t incl = lb;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const uint64_t start = P.off[s] + (incl - lb);
+    const uint32_t r = (uint32_t)(start & 31);
+    const uint64_t w0 = start >> 5;
+    const uint32_t nsrc = (lb + 31) >> 5;
+    const uint32_t ndst = lb ? (uint32_t)(((start + lb - 1) >> 5) - w0 + 1) : 0u;
+    const uint32_t* src = slot + s * (uint64_t)lcap * 64 + lane;
+    // next lane: does it start inside my last word?  (lane 63's successor is the next segment)
+    const uint32_t nlb = __shfl_down(lb, 1, 64);
+    const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
+    const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
+    uint32_t prev = 0, first = 0, last = 0;
+    for (uint32_t d = 0; d < ndst; d++) {
+        const uint32_t cur = d < nsrc ? src[(size_t)d * 64] : 0u;
+        const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
+        prev = cur;
+        if (d == 0) first = v;
+        if (d == ndst - 1) last = v;
+        if (d != 0 && d != ndst - 1) P.out[w0 + d] = __builtin_bswap32(v);
+    }
+    const uint32_t nfirst = __shfl_down(first, 1, 64);
+    if (next_shares) last |= nfirst;  // ndst == 1 only when r == 0 and lb == 32: never shared then
+    if (ndst == 0) return;
+    const bool shares_prev = lane > 0 && r != 0;  // my first word belongs to lane - 1's last store
+    if (ndst == 1) {
+        if (lane == 0) P.head[s] = __builtin_bswap32(first);
+        else if (last_lane) P.tail[s] = __builtin_bswap32(last);
+        else P.out[w0] = __builtin_bswap32(last);
+        return;
+    }
+    if (lane == 0) P.head[s] = __builtin_bswap32(first);
+    else if (!shares_prev) P.out[w0] = __builtin_bswap32(first);
+    if (last_lane) P.tail[s] = __builtin_bswap32(last);
+    else P.out[w0 + ndst - 1] = __builtin_bswap32(last);
+}
+
 // =================================================================================================
 // Decode: the inverse of the stream above (expGolomb_readValue, ExpGolomb.c:66-110 /
 // ExpGolombReader.java:19-63; Decoder.java:78-96 places value i of a cube at diagonal position i).
@@ -416,6 +469,17 @@ int launch_eg_scan(const EgParams& P, hipStream_t st) {
     hipLaunchKernelGGL(eg_scan_reduce_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
     hipLaunchKernelGGL(eg_scan_top_kernel, dim3(1), dim3(1024), 0, st, P, (uint32_t)n_chunks);
     hipLaunchKernelGGL(eg_scan_apply_kernel, dim3((uint32_t)n_chunks), dim3(kEgBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_eg_compact(int D, const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t lcap,
+                      hipStream_t st) {
+    (void)D;
+    if (P.n_cubes == 0) return 0;
+    if (launch_eg_scan(P, st)) return -1;
+    const uint64_t blocks = (P.n_cubes + kEgWaves - 1) / kEgWaves;
+    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, lane_bits, lcap);
+    hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

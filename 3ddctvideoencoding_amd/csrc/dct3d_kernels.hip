@@ -407,17 +407,73 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
 // =============================================================================================
 // Exact Java fold for flagged (cube, k): out = JavaRound(fold_g(S_g * coef_g) / step)
 // =============================================================================================
+// The Java fold of DCT.java:44-52 for coefficient k of cube g, by one whole wave:
+//   out = sum over groups gi (HashMap order) of  S_gi * coef_gi,  S_gi = exact integer pixel sums.
+// Group sums: LDS integer atomics (exact).  Products: one lane per group, in parallel (each is one
+// correctly rounded fp64 multiply, as in Java).  The fold itself (the only order-dependent part) runs
+// on lane 0 over the products in LDS.  ssum / prod: the wave's kMaxGroupsDev-entry scratch.  The
+// result is valid in lane 0.
+struct ReplayGeom {
+    const uint8_t* raster;
+    uint32_t cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+    const int32_t* ngroups;
+    const double* coef;
+    const uint8_t* group_of;
+};
+template <int D>
+__device__ __forceinline__ int exact_coef(const ReplayGeom& R, uint32_t g, uint32_t k, int lane, int* ssum,
+                                          double* prod) {
+    constexpr int CS = 64 * D;
+    const int ng = R.ngroups[k];
+    const double cf = lane < ng ? R.coef[(size_t)k * kMaxGroupsDev + lane] : 0.0;  // issued early
+    ssum[lane] = 0;
+    wave_lds_sync();
+    if (lane * 8 < CS) {
+        const int z = lane >> 3, y = lane & 7;
+        const uint32_t s = g / R.cubes_per_stack;
+        const uint32_t r = g - s * R.cubes_per_stack;
+        const uint32_t by = r / R.nbx, bx = r - by * R.nbx;
+        const uint8_t* src = R.raster + (size_t)s * R.stack_stride + (size_t)z * R.plane +
+                             (size_t)(by * 8 + y) * R.width + bx * 8;
+        const uint2 px = *(const uint2*)src;
+        const uint2 gr = *(const uint2*)(R.group_of + (size_t)k * CS + lane * 8);
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const uint32_t g0 = (gr.x >> (8 * bb)) & 0xFF, g1 = (gr.y >> (8 * bb)) & 0xFF;
+            if (g0 < kMaxGroupsDev) atomicAdd(&ssum[g0], (int)((px.x >> (8 * bb)) & 0xFF));
+            if (g1 < kMaxGroupsDev) atomicAdd(&ssum[g1], (int)((px.y >> (8 * bb)) & 0xFF));
+        }
+    }
+    wave_lds_sync();
+    prod[lane] = __dmul_rn((double)ssum[lane], cf);
+    wave_lds_sync();
+    int q = 0;
+    if (lane == 0) {
+        double acc = 0.0;
+        int gi = 0;
+        for (; gi + 4 <= ng; gi += 4) {  // DCT.java:50, output += sum * coefficient, in order
+            const double p0 = prod[gi], p1 = prod[gi + 1], p2 = prod[gi + 2], p3 = prod[gi + 3];
+            acc = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(acc, p0), p1), p2), p3);
+        }
+        for (; gi < ng; gi++) acc = __dadd_rn(acc, prod[gi]);
+        const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+        const int st = max(1, 5 * (kx + ky + kz));
+        q = java_round_dev(__ddiv_rn(acc, (double)st));
+    }
+    wave_lds_sync();
+    return q;
+}
+
+// One wave per uncertified coefficient (flag list), then every coefficient of the whole-cube list.
 template <int D>
 __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
-    // One wave per uncertified coefficient (cube g, index k): the Java fold of DCT.java:44-52,
-    //   out = sum over groups gi (HashMap order) of  S_gi * coef_gi,  S_gi = exact integer pixel sums.
-    // Group sums: LDS integer atomics (exact).  Products: one lane per group, in parallel (each is one
-    // correctly rounded fp64 multiply, as in Java).  The fold itself (the only order-dependent part)
-    // runs on lane 0 over the products in LDS.
     constexpr int CS = 64 * D;
     __shared__ int Ssum[4][kMaxGroupsDev];
     __shared__ double prod[4][kMaxGroupsDev];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
+                       P.ngroups, P.coef, P.group_of};
     const uint32_t nf = min(P.counters[0], P.flag_cap);
     const uint32_t ncube = P.counters[1];
     const unsigned long long total = (unsigned long long)nf + (unsigned long long)ncube * CS;
@@ -433,44 +489,174 @@ __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
             g = P.cube_list[e2 / CS];
             k = (uint32_t)(e2 % CS);
         }
-        const int ng = P.ngroups[k];
-        const double cf = lane < ng ? P.coef[(size_t)k * kMaxGroupsDev + lane] : 0.0;  // issued early
-        Ssum[wave][lane] = 0;
-        wave_lds_sync();
-        if (lane * 8 < CS) {
-            const int z = lane >> 3, y = lane & 7;
-            const uint32_t s = g / P.cubes_per_stack;
-            const uint32_t r = g - s * P.cubes_per_stack;
-            const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
-            const uint8_t* src = P.raster + (size_t)s * P.stack_stride + (size_t)z * P.plane +
-                                 (size_t)(by * 8 + y) * P.width + bx * 8;
-            const uint2 px = *(const uint2*)src;
-            const uint2 gr = *(const uint2*)(P.group_of + (size_t)k * CS + lane * 8);
-#pragma unroll
-            for (int bb = 0; bb < 4; bb++) {
-                const uint32_t g0 = (gr.x >> (8 * bb)) & 0xFF, g1 = (gr.y >> (8 * bb)) & 0xFF;
-                if (g0 < kMaxGroupsDev) atomicAdd(&Ssum[wave][g0], (int)((px.x >> (8 * bb)) & 0xFF));
-                if (g1 < kMaxGroupsDev) atomicAdd(&Ssum[wave][g1], (int)((px.y >> (8 * bb)) & 0xFF));
-            }
-        }
-        wave_lds_sync();
-        prod[wave][lane] = __dmul_rn((double)Ssum[wave][lane], cf);
-        wave_lds_sync();
-        if (lane == 0) {
-            double acc = 0.0;
-            int gi = 0;
-            for (; gi + 4 <= ng; gi += 4) {  // DCT.java:50, output += sum * coefficient, in order
-                const double p0 = prod[wave][gi], p1 = prod[wave][gi + 1], p2 = prod[wave][gi + 2],
-                             p3 = prod[wave][gi + 3];
-                acc = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(acc, p0), p1), p2), p3);
-            }
-            for (; gi < ng; gi++) acc = __dadd_rn(acc, prod[wave][gi]);
-            const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-            const int st = max(1, 5 * (kx + ky + kz));
-            P.out[(size_t)g * CS + k] = java_round_dev(__ddiv_rn(acc, (double)st));
-        }
-        wave_lds_sync();
+        const int q = exact_coef<D>(R, g, k, lane, Ssum[wave], prod[wave]);
+        if (lane == 0) P.out[(size_t)g * CS + k] = q;
     }
+}
+
+// =============================================================================================
+// Fused encode + Exp-Golomb, K1 (dct3d_encode_eg_dev; encoder.c:228-296 up to the deflate)
+// =============================================================================================
+// The wave's 8 cubes: rows -> transform -> quantise + certify exactly as encode_body, but the
+// uncertified coefficients are recorded in a per-lane bit mask (bit ky*NB + x) and replayed by the
+// wave itself (exact_coef) after the quantised cubes are staged in LDS as int16 (|q| <= 255*sqrt(cs)
+// by Parseval, DC included).  Then lane (c', part) codes stream positions part*VPL .. part*VPL+VPL-1
+// of cube c' (diagonal-slice order, CubeUtils.c:5-46; signed order-0 Exp-Golomb, ExpGolomb.c:32-64)
+// into its own words of the segment's slot; eg_compact_kernel later concatenates the lanes.
+template <int D>
+__global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, EgFusedParams E) {
+    constexpr int CS = 64 * D;
+    constexpr int NB = (D == 8) ? 8 : 4;
+    constexpr int NI = 7 + NB;
+    constexpr int VPL = CS / 8;            // stream values per lane
+    constexpr int CUBE_B = 2 * CS + 16;    // int16 cube-major staging per cube (+16 B: bank spread)
+    static_assert(8 * CUBE_B <= kWaveLds, "int16 staging must fit the wave region");
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+    __shared__ int rs_sum[kWavesPerBlock][kMaxGroupsDev];
+    __shared__ double rs_prod[kWavesPerBlock][kMaxGroupsDev];
+    __shared__ __attribute__((aligned(16))) uint16_t s_pos[CS];  // stream position -> byte offset in a cube
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t wid = blockIdx.x * kWavesPerBlock + wave;  // segment index
+    const uint32_t cube0 = wid * kCubesPerWave;
+    uint2 raw[D];
+    load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
+    for (int i = threadIdx.x; i < CS; i += kBlock) s_pos[i] = (uint16_t)(2 * E.diag[i]);
+    __syncthreads();
+    if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
+    char* wl = lds + wave * kWaveLds;
+    const int c = lane >> 3, j = lane & 7;
+    const int kz = (D == 8) ? j : (j >> 1);
+    const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
+    const int so = kz + kx0;
+    const bool valid = cube0 + c < P.n_cubes;
+
+    float a[D][8];
+    to_float<D>(raw, a);
+    uint32_t S;
+    int m;
+    float A;
+    cube_stats<D>(raw, a, S, m, A);
+    asm volatile("" : "+v"(S), "+v"(m), "+v"(A));
+    float b[8][NB];
+    forward_cube<D, NB>(a, m, c, j, wl, b);
+
+    int sz = so;
+    asm volatile("" : "+v"(sz));
+    float rr[NI], thr[NI];
+#pragma unroll
+    for (int i = 0; i < NI; i++) {
+        rr[i] = P.tab_rstep[sz + i];
+        thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
+    }
+    int32_t qv[8][NB];
+    uint32_t fm_lo = 0, fm_hi = 0;  // uncertified mask: bit ky*NB + x (64 bits for NB = 8)
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++) {
+        pin(b[ky]);
+        bool f = false;
+        float qq[NB];
+#pragma unroll
+        for (int x = 0; x < NB; x++) {
+            qq[x] = b[ky][x] * rr[ky + x];
+            const float n = __builtin_rintf(qq[x]);
+            f |= __builtin_fabsf(qq[x] - n) >= thr[ky + x];
+            qv[ky][x] = (int32_t)n;
+        }
+        if (__builtin_expect(f, 0)) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int x = 0; x < NB; x++)
+                if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) bits |= 1u << x;
+            const int sh = ky * NB;
+            if (sh < 32) fm_lo |= bits << sh;
+            else fm_hi |= bits << (sh - 32);
+        }
+        pin(qv[ky]);
+        asm volatile("" : "+v"(fm_lo), "+v"(fm_hi));
+    }
+    if (j == 0) {
+        qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+        fm_lo &= ~1u;
+    }
+    if (!valid) fm_lo = fm_hi = 0;
+
+    // stage the cubes as int16, cube-major (k = (kz*8 + ky)*8 + kx at byte 2k of cube c)
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++) {
+        char* row = wl + c * CUBE_B + 2 * ((kz * 8 + ky) * 8 + kx0);
+        if constexpr (D == 8) {
+            *(uint4*)row = make_uint4(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
+                                      __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u),
+                                      __builtin_amdgcn_perm(qv[ky][5], qv[ky][4], 0x05040100u),
+                                      __builtin_amdgcn_perm(qv[ky][7], qv[ky][6], 0x05040100u));
+        } else {
+            *(uint2*)row = make_uint2(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
+                                      __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u));
+        }
+    }
+    wave_lds_sync();
+
+    // exact replay of the uncertified coefficients, one at a time by the whole wave (rare)
+    {
+        const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
+                           E.ngroups, E.coef, E.group_of};
+        for (;;) {
+            const unsigned long long who = __ballot((fm_lo | fm_hi) != 0u);
+            if (who == 0ull) break;
+            const int src = __builtin_ctzll(who);
+            const int mybit = fm_lo ? __builtin_ctz(fm_lo) : (fm_hi ? 32 + __builtin_ctz(fm_hi) : 0);
+            const int bit = __shfl(mybit, src, 64);
+            const int sj = src & 7, sc = src >> 3;
+            const int skz = (D == 8) ? sj : (sj >> 1), skx0 = (D == 8) ? 0 : (sj & 1) * 4;
+            const uint32_t k = (uint32_t)((skz * 8 + bit / NB) * 8 + skx0 + bit % NB);
+            const int q = exact_coef<D>(R, cube0 + sc, k, lane, rs_sum[wave], rs_prod[wave]);
+            if (lane == 0) *(int16_t*)(wl + sc * CUBE_B + 2 * k) = (int16_t)q;
+            if (lane == src) {
+                if (fm_lo) fm_lo &= fm_lo - 1;
+                else fm_hi &= fm_hi - 1;
+            }
+            wave_lds_sync();
+        }
+    }
+
+    // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp; a 64-bit
+    // accumulator, one MSB-first word out whenever 32 bits are pending (width <= 27 + 31 pending)
+    const int cp = lane >> 3, part = lane & 7;
+    const bool lvalid = cube0 + cp < P.n_cubes;
+    const char* cb = wl + cp * CUBE_B;
+    uint32_t* dst = E.slot + (size_t)wid * E.lcap * 64 + lane;
+    uint64_t acc = 0;
+    uint32_t nb = 0, nw = 0;
+    if (lvalid) {
+#pragma unroll 1
+        for (int i0 = 0; i0 < VPL; i0 += 8) {
+            const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
+            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+            int v[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) v[e] = *(const int16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t ng = (uint32_t)(-v[e]);
+                const uint32_t code = ((ng << 1) ^ (uint32_t)((int32_t)ng >> 31)) + 1u;  // v<=0: 1-2v, v>0: 2v
+                const uint32_t width = 63u - 2u * (uint32_t)__clz((int)code);
+                acc = (acc << width) | code;
+                nb += width;
+                if (nb >= 32u) {
+                    nb -= 32u;
+                    dst[(size_t)nw * 64] = (uint32_t)(acc >> nb);
+                    nw++;
+                }
+            }
+        }
+        if (nb) dst[(size_t)nw * 64] = (uint32_t)(acc << (32u - nb));
+    }
+    const uint32_t lbits = lvalid ? nw * 32u + nb : 0u;
+    E.lane_bits[(size_t)wid * 64 + lane] = (uint16_t)lbits;
+    uint32_t tot = lbits;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane == 0) E.seg_bits[wid] = tot;
 }
 
 // =============================================================================================
@@ -1030,6 +1216,12 @@ void launch_enc_t(const EncodeParams& P, hipStream_t st) {
     hipLaunchKernelGGL((encode_kernel<D, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
 }
 template <int D>
+void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
+    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
+    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+}
+template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
     switch (v) {
         case 0: launch_enc_t<D, false>(P, st); break;
@@ -1048,6 +1240,13 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     }
     if (D == 8) launch_enc_variant<8>(variant, P, st);
     else launch_enc_variant<4>(variant, P, st);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
+    if (P.n_cubes == 0) return 0;
+    if (D == 8) launch_enc_eg_t<8>(P, E, st);
+    else launch_enc_eg_t<4>(P, E, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

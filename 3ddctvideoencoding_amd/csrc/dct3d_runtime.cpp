@@ -68,6 +68,8 @@ struct dct3d_ctx {
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
+    // fused encode + Exp-Golomb: per-segment lane slots and lane bit counts
+    DevBuf d_egf_slot, d_egf_lbits;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster;
     uint64_t eg_last_bytes = 0;
@@ -579,6 +581,83 @@ int dct3d_eg_encode_dev(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint
     return eg_run(c, d_q, n_cubes, carry_byte, carry_bits, (uint32_t*)d_out, out_cap, total_bits);
 }
 
+// Fused device path: encode_eg_kernel (transform, quantise, in-wave exact replay, lane-level
+// Exp-Golomb into slots) -> scan over segments -> eg_compact_kernel -> eg_stitch_kernel.
+int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, uint8_t carry_byte,
+                        int carry_bits, uint8_t* d_out, uint64_t out_cap, uint64_t* total_bits) {
+    if (!c || (!d_raster && n_stacks) || carry_bits < 0 || carry_bits > 7 || ((uintptr_t)d_out & 3)) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    c->last_valid = false;
+    if (n_cubes == 0) return dct3d_eg_encode_dev(c, nullptr, 0, carry_byte, carry_bits, d_out, out_cap, total_bits);
+    if (!d_out) return DCT3D_EINVAL;
+    const int D = c->bd;
+    const uint64_t n_seg = (n_cubes + 7) / 8, n_chunks = (n_seg + 4095) / 4096;
+    const uint32_t lcap = (uint32_t)((c->plan.cs / 8) * 27 + 31) / 32;  // cs/8 values x <= 27 bits
+    if ((rc = c->d_egf_slot.grow(n_seg * lcap * 64 * sizeof(uint32_t))) ||
+        (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
+        (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
+        (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
+        return rc;
+    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    const uint64_t plane = (uint64_t)w * h;
+    EncodeParams P{};
+    P.raster = d_raster;
+    P.out = nullptr;
+    P.n_cubes = (uint32_t)n_cubes;
+    P.g_base = 0;
+    P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
+    P.nbx = (uint32_t)(w / 8);
+    P.width = (uint32_t)w;
+    P.plane = plane;
+    P.stack_stride = plane * D;
+    P.coef_dc = c->plan.coef_dc;
+    const float* tabs = (const float*)c->d_tabs.p;
+    P.tab_rstep = tabs;
+    P.tab_G = tabs + kMaxS;
+    P.tab_E = tabs + 2 * kMaxS;
+    EgFusedParams E;
+    E.ngroups = (const int32_t*)c->d_ngroups.p;
+    E.coef = (const double*)c->d_coef.p;
+    E.group_of = (const uint8_t*)c->d_group_of.p;
+    E.diag = (const uint16_t*)c->d_diag.p;
+    E.slot = (uint32_t*)c->d_egf_slot.p;
+    E.lcap = lcap;
+    E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
+    E.seg_bits = (uint32_t*)c->d_eg_bits.p;
+    hipEvent_t* ev = timing_slot(c);
+    if (ev) (void)hipEventRecord(ev[0], c->stream);
+    if (launch_encode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    EgParams G;
+    G.q = nullptr;
+    G.n_cubes = n_seg;  // segments
+    G.diag = E.diag;
+    G.bits = E.seg_bits;
+    G.off = (uint64_t*)c->d_eg_off.p;
+    G.bsum = (uint64_t*)c->d_eg_bsum.p;
+    G.status = (uint64_t*)c->d_eg_status.p;
+    G.head = (uint32_t*)c->d_eg_ht.p;
+    G.tail = (uint32_t*)c->d_eg_ht.p + n_seg;
+    G.out = (uint32_t*)d_out;
+    G.out_cap_words = out_cap / 4;
+    G.carry_bits = (uint32_t)carry_bits;
+    G.carry_byte = carry_byte;
+    if (ev) (void)hipEventRecord(ev[2], c->stream);
+    if (launch_eg_compact(D, G, E.slot, E.lane_bits, lcap, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    uint64_t st[2] = {0, 0};
+    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    if (total_bits) *total_bits = st[0];
+    c->last_units = n_cubes * (uint64_t)c->plan.cs;
+    if (st[1] & 1) return DCT3D_ENOSPC;
+    return DCT3D_OK;
+}
+
 int dct3d_encode_eg(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n_stacks, uint8_t carry_byte,
                     int carry_bits, uint64_t* total_bits) {
     if (!c || (!raster && n_stacks) || carry_bits < 0 || carry_bits > 7) return DCT3D_EINVAL;
@@ -592,6 +671,24 @@ int dct3d_encode_eg(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n_sta
         return rc;
     if (n_cubes && hipMemcpyAsync(c->h_in.p, raster, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
+    static const bool two_step = [] {  // A/B knob: encode to int32 cube-major, then the stand-alone EG stage
+        const char* e = getenv("DCT3D_EG_TWO_STEP");
+        return e && atoi(e) != 0;
+    }();
+    if (!two_step) {
+        uint64_t cap = in_bytes + 64, tb = 0;
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if ((rc = c->d_eg_out.grow(cap))) return rc;
+            rc = dct3d_encode_eg_dev(c, (const uint8_t*)c->h_in.p, w, h, n_stacks, carry_byte, carry_bits,
+                                     (uint8_t*)c->d_eg_out.p, c->d_eg_out.bytes, &tb);
+            if (rc != DCT3D_ENOSPC) break;
+            cap = (tb + 31) / 32 * 4 + 64;
+        }
+        if (rc) return rc;
+        if (total_bits) *total_bits = tb;
+        c->eg_last_bytes = (tb + 7) / 8;
+        return DCT3D_OK;
+    }
     if (n_cubes && (rc = dct3d_encode_stacks_dev(c, (const uint8_t*)c->h_in.p, w, h, n_stacks, (int32_t*)c->d_eg_q.p, nullptr)))
         return rc;
     // first try: 1 byte per value (8 bits / value; typical content needs 1.5-4), grown to fit on ENOSPC

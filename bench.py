@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true")
+    ap.add_argument("--eg-two-step", action="store_true",
+                    help="c7: encode to int32 cube-major, then the stand-alone Exp-Golomb stage (A/B)")
     return ap.parse_args()
 
 
@@ -165,7 +167,7 @@ def main():
 
         def step():
             ctx.decode_stacks_dev(q, width, height, stacks, out)
-    elif direction == "encode_eg":
+    elif direction == "encode_eg" and a.eg_two_step:
         eg_cap = n_cubes * cs  # 8 bits per value: far above what quantised content needs
         eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
         eg_ev = []
@@ -177,6 +179,15 @@ def main():
             eg_info["bits"] = ctx.eg_encode_dev(q, n_cubes, eg_out, eg_cap)  # synchronises (total read back)
             e1.record()
             eg_ev.append((e0, e1))
+    elif direction == "encode_eg":
+        # fused path (dct3d_encode_eg_dev): raster -> stream, no int32 intermediate
+        eg_cap = n_cubes * cs
+        eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
+        del q
+        q = None
+
+        def step():
+            eg_info["bits"] = ctx.encode_eg_dev(frames, width, height, stacks, eg_out, eg_cap)  # synchronises
     else:
         def step():
             ctx.encode_stacks_dev(frames, width, height, stacks, q)
@@ -199,17 +210,20 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
     ctx.set_profiling(False)
-    ceiling = None if a.no_ceiling else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
+    ceiling = None if a.no_ceiling or q is None else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
     sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
     elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
 
     ms_per_step = elapsed * 1e3 / a.steps
     value = total_cubes * a.steps / elapsed
     bytes_per_cube = cs * (1 + 4)  # u8 in + int32 out (encode) / int32 in + u8 out (decode)
+    fused = direction == "encode_eg" and not a.eg_two_step
+    if fused:  # u8 in + the cube's share of the coded stream, lane bit counts and segment totals out
+        bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes + (64 * 2 + 4) / 8
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
     fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
     achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
-    kname = "decode_kernel" if direction == "decode" else "encode_kernel"
+    kname = "decode_kernel" if direction == "decode" else ("encode_eg_kernel" if fused else "encode_kernel")
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
@@ -254,7 +268,8 @@ def main():
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,
         "eg_stage": None if direction != "encode_eg" else {
-            "ms_per_step": sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps,
+            "path": "fused" if fused else "two-step",
+            "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
             "bits_per_value": eg_info["bits"] / (n_cubes * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
         "cpu_baseline": None,

@@ -59,7 +59,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written to it) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 2
+#define DCT3D_ABI_VERSION 3
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -185,6 +185,16 @@ int dct3d_eg_encode_dev(dct3d_ctx *ctx, const int32_t *d_q, uint64_t n_cubes, ui
  * of the raw bytes.  *total_bits as above; fetch the bytes with dct3d_eg_fetch. */
 int dct3d_encode_eg(dct3d_ctx *ctx, const uint8_t *raster, int width, int height, int n_stacks, uint8_t carry_byte,
                     int carry_bits, uint64_t *total_bits);
+
+/* Device raster in, device stream out, fused: encoder.c:228-296 up to the deflate
+ * (readCubes + DCT + quantisation + applyExpGolombCoding) for n_stacks stacks of d_raster, without
+ * the int32 cube-major intermediate -- uncertified coefficients are replayed exactly inside the
+ * transform kernel, and each wave codes its 8 cubes straight into the stream.  The stream format,
+ * carry, d_out and *total_bits are those of dct3d_eg_encode_dev (the bytes are identical to
+ * dct3d_encode_stacks_dev followed by dct3d_eg_encode_dev).  DCT3D_ENOSPC when out_cap is too small
+ * (*total_bits is still set).  Synchronises the context stream. */
+int dct3d_encode_eg_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
+                        uint8_t carry_byte, int carry_bits, uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
 
 /* Copies the first `nbytes` bytes of the last dct3d_encode_eg stream to host memory. */
 int dct3d_eg_fetch(dct3d_ctx *ctx, uint8_t *out, uint64_t nbytes);

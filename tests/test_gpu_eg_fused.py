@@ -1,0 +1,126 @@
+"""GPU: the fused encode + Exp-Golomb path (dct3d_encode_eg_dev).
+
+The stream must be the reference's (encoder.c:228-296 up to the deflate: DCT + quantisation +
+diagonal-slice order + signed order-0 Exp-Golomb, one continuous bitstream carrying the partial byte)
+bit for bit.  Expected streams: the oracle's quantised cubes (plan.encode_q, the restated Java
+DCT.java / Encoder.java) through the oracle's Exp-Golomb writer at sizes the oracle finishes in
+seconds, and the two-step device path (dct3d_encode_stacks_dev + dct3d_eg_encode_dev, both pinned
+against the oracle in test_gpu_parity.py / test_gpu_eg.py) at 1080p."""
+import numpy as np
+import pytest
+
+from test_gpu_eg import _expected, _gpu_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _fused(ctx, fr, carry_byte=0, carry_bits=0, cap=None):
+    import torch
+    fr = np.ascontiguousarray(fr, np.uint8)
+    F, H, W = fr.shape
+    d = torch.from_numpy(fr).cuda()
+    cap = cap if cap is not None else (fr.size * 4 + 64) // 4 * 4
+    out = torch.zeros(cap // 4 + 1, dtype=torch.int32, device="cuda")
+    tb = ctx.encode_eg_dev(d, W, H, F // ctx.bd, out, cap, carry_byte, carry_bits)
+    raw = out.cpu().numpy().view(np.uint8)
+    return raw[: (tb + 7) // 8].tobytes(), tb, raw
+
+
+def _content(pkg, kind, w, h, f):
+    if kind in ("ramp", "uniform"):
+        return pkg.synthetic.frames(w, h, f, kind=kind)
+    if kind == "zeros":
+        return np.zeros((f, h, w), np.uint8)
+    if kind == "full":
+        return np.full((f, h, w), 255, np.uint8)
+    if kind == "checker":   # extreme AC coefficients (largest codes)
+        z, y, x = np.indices((f, h, w))
+        return (((x + y + z) & 1) * 255).astype(np.uint8)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["ramp", "uniform", "zeros", "full", "checker"])
+def test_fused_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, kind):
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    fr = _content(pkg, kind, 64, 64, 2 * depth)
+    exp, ebits = _expected(oracle, pkg, plan.encode_q(fr), depth)
+    got, tb, raw = _fused(ctx, fr)
+    assert tb == ebits
+    assert got == exp
+    assert not raw[len(got):(tb + 31) // 32 * 4].any()      # zero padding to the word
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("w,h,stacks", [(8, 8, 1), (24, 16, 3), (40, 8, 5), (136, 72, 2)])
+def test_fused_ragged_segment_tails(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, w, h, stacks):
+    """cube counts that are not a multiple of 8: the last wave codes a partial segment"""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    fr = pkg.synthetic.frames(w, h, stacks * depth, kind="uniform", frame0=w + h)
+    exp, ebits = _expected(oracle, pkg, plan.encode_q(fr), depth)
+    got, tb, _ = _fused(ctx, fr)
+    assert tb == ebits and got == exp
+
+
+@pytest.mark.parametrize("carry_bits", range(8))
+def test_fused_carry_partial_byte(pkg, oracle, plan8, gpu_ctx8, carry_bits):
+    fr = pkg.synthetic.frames(48, 40, 8, kind="uniform", frame0=carry_bits)
+    exp, ebits = _expected(oracle, pkg, plan8.encode_q(fr), 8, 0x5A, carry_bits)
+    got, tb, _ = _fused(gpu_ctx8, fr, 0x5A, carry_bits)
+    assert tb == ebits and got == exp
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["ramp", "uniform"])
+def test_fused_1080p_matches_two_step(pkg, gpu_ctx8, gpu_ctx4, depth, kind):
+    """1080p, 2 stacks: uncertified coefficients (uniform content, 8x8x4 exact ties) replayed inside
+    the fused kernel must give the fixup kernel's values"""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = pkg.synthetic.frames(1920, 1080, 2 * depth, kind=kind)
+    q = ctx.encode_stacks(fr)
+    ref, rbits, _ = _gpu_stream(ctx, q)
+    got, tb, _ = _fused(ctx, fr)
+    assert tb == rbits and got == ref
+
+
+def test_fused_1080p_matches_oracle(pkg, oracle, plan8, gpu_ctx8):
+    fr = pkg.synthetic.frames(1920, 1080, 8, kind="ramp", frame0=3)
+    exp, ebits = _expected(oracle, pkg, plan8.encode_q(fr), 8)
+    got, tb, _ = _fused(gpu_ctx8, fr)
+    assert tb == ebits and got == exp
+
+
+def test_fused_capacity(pkg, gpu_ctx8):
+    fr = pkg.synthetic.frames(64, 64, 8, kind="uniform")
+    _, tb, _ = _fused(gpu_ctx8, fr)
+    import torch
+    d = torch.from_numpy(np.ascontiguousarray(fr)).cuda()
+    small = (tb // 32) * 4 - 4          # one word short
+    out = torch.full((small // 4 + 4,), 7, dtype=torch.int32, device="cuda")
+    with pytest.raises(pkg.Dct3dError) as ei:
+        gpu_ctx8.encode_eg_dev(d, 64, 64, 1, out, small)
+    assert ei.value.code == pkg.DCT3D_ENOSPC
+    assert (out.cpu().numpy() == 7).all()          # nothing written
+    got, tb2, _ = _fused(gpu_ctx8, fr, cap=(tb + 31) // 32 * 4)   # exactly enough
+    assert tb2 == tb
+
+
+def test_fused_empty_and_errors(pkg, gpu_ctx8):
+    import torch
+    out = torch.zeros(4, dtype=torch.int32, device="cuda")
+    d = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    assert gpu_ctx8.encode_eg_dev(d, 8, 8, 0, out, 16, 0xF0, 4) == 4
+    assert out.cpu().numpy().view(np.uint8)[0] == 0xF0
+    with pytest.raises(pkg.Dct3dError):
+        gpu_ctx8.encode_eg_dev(d, 12, 8, 1, out, 16)     # width not a multiple of the block width
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_host_encode_eg_is_fused_and_identical(pkg, gpu_ctx8, gpu_ctx4, depth):
+    """dct3d_encode_eg (host raster in) now runs the fused path; its stream equals the two-step one"""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = pkg.synthetic.frames(320, 240, 3 * depth, kind="ramp", frame0=11)
+    q = ctx.encode_stacks(fr)
+    ref, rbits, _ = _gpu_stream(ctx, q, 0x80, 1)
+    got, tb = ctx.encode_eg(fr, 0x80, 1)
+    assert tb == rbits and got == ref
