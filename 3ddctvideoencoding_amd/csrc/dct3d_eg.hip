@@ -255,37 +255,46 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
     if (g + 1 == P.n_cubes || (end >> 5) != wl) P.out[wl] = P.tail[g];
 }
 
-// Fused path, K3: one wave per segment (8 cubes, coded by encode_eg_kernel into lane-interleaved
-// slot words).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are shifted
-// into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane has
-// >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
-// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.
+// Fused path, K3: one wave per segment (8 cubes coded by encode_eg_kernel, lane l's words at rows
+// i*64 + l of the slot).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
+// shifted into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane
+// has >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
+// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.  The first 4 rows are loaded
+// before any is used (typical content needs <= 3 words per lane).
 __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
-                                                              const uint16_t* __restrict__ lane_bits, uint32_t lcap) {
+                                                              const uint16_t* __restrict__ lane_bits, uint32_t seg_cap) {
     if (P.status[1] != 0) return;  // capacity failure: nothing is written
     const int lane = threadIdx.x & 63;
     const uint64_t s = (uint64_t)blockIdx.x * kEgWaves + (threadIdx.x >> 6);
     if (s >= P.n_cubes) return;
+    const uint32_t* src = slot + s * (uint64_t)seg_cap + lane;
+    // independent loads, one round trip: the first 4 rows unconditionally (a slot has >= 27 rows;
+    // words past a lane's last one are never used), its bit count, the segment offset
+    uint32_t pre[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) pre[t] = src[t * 64];
     const uint32_t lb = lane_bits[s * 64 + lane];
+    const uint64_t base = P.off[s];
+    const uint32_t nsrc = (lb + 31) >> 5;
     uint32_t incl = lb;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t t = __shfl_up(incl, o, 64);
         if (lane >= o) incl += t;
     }
-    const uint64_t start = P.off[s] + (incl - lb);
+    const uint64_t start = base + (incl - lb);
     const uint32_t r = (uint32_t)(start & 31);
     const uint64_t w0 = start >> 5;
-    const uint32_t nsrc = (lb + 31) >> 5;
     const uint32_t ndst = lb ? (uint32_t)(((start + lb - 1) >> 5) - w0 + 1) : 0u;
-    const uint32_t* src = slot + s * (uint64_t)lcap * 64 + lane;
-    // next lane: does it start inside my last word?  (lane 63's successor is the next segment)
     const uint32_t nlb = __shfl_down(lb, 1, 64);
     const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
     const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
     uint32_t prev = 0, first = 0, last = 0;
     for (uint32_t d = 0; d < ndst; d++) {
-        const uint32_t cur = d < nsrc ? src[(size_t)d * 64] : 0u;
+        uint32_t cur;
+        if (d >= nsrc) cur = 0u;
+        else if (d < 4) cur = d == 0 ? pre[0] : d == 1 ? pre[1] : d == 2 ? pre[2] : pre[3];
+        else cur = src[(size_t)d * 64];
         const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
         prev = cur;
         if (d == 0) first = v;
@@ -472,13 +481,12 @@ int launch_eg_scan(const EgParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_compact(int D, const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t lcap,
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,
                       hipStream_t st) {
-    (void)D;
     if (P.n_cubes == 0) return 0;
     if (launch_eg_scan(P, st)) return -1;
     const uint64_t blocks = (P.n_cubes + kEgWaves - 1) / kEgWaves;
-    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, lane_bits, lcap);
+    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, lane_bits, seg_cap);
     hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -112,25 +112,25 @@ struct EgDecParams {
 
 // Fused encode + Exp-Golomb (dct3d_encode_eg_dev): the encode kernel's transform / quantise /
 // certify, the exact Java replay of uncertified coefficients inside the wave, then the wave's 8
-// cubes coded straight from registers / LDS into a private slot (no int32 cube-major round trip).
-// Segment = one wave = 8 consecutive cubes; each lane codes 1/8 of one cube's diagonal stream.
+// cubes coded straight into a private slot (no int32 cube-major round trip).  Segment = one wave = 8
+// consecutive cubes; lane l codes 1/8 of one cube's diagonal stream into its words of the slot.
 struct EgFusedParams {
     const int32_t* ngroups;    // exact replay tables (as FixupParams)
     const double* coef;
     const uint8_t* group_of;
     const uint16_t* diag;      // [cs] stream position -> cube index
-    uint32_t* slot;            // per segment lcap * 64 words, lane-interleaved (word i of lane l at i*64 + l),
-                               // MSB-first stream words, each lane's first bit at bit 31 of its word 0
-    uint32_t lcap;             // words per lane (worst case: cs/8 values x 27 bits)
+    uint32_t* slot;            // [n_seg * seg_cap]: word i of lane l at i*64 + l, MSB-first, each lane's
+                               // first bit at bit 31 of its word 0
+    uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
     uint16_t* lane_bits;       // [n_seg * 64] bits coded by each lane
     uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
 };
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
 int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st);
-// scan of the segment bits + compaction of the lane slots into the stream + stitch (P.n_cubes =
+// scan of the segment bits + the lanes' words concatenated into the stream + stitch (P.n_cubes =
 // segments, P.bits = seg_bits)
-int launch_eg_compact(int D, const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t lcap,
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,
                       hipStream_t st);
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st);

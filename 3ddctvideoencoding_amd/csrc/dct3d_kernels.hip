@@ -503,6 +503,16 @@ __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
 // by Parseval, DC included).  Then lane (c', part) codes stream positions part*VPL .. part*VPL+VPL-1
 // of cube c' (diagonal-slice order, CubeUtils.c:5-46; signed order-0 Exp-Golomb, ExpGolomb.c:32-64)
 // into its own words of the segment's slot; eg_compact_kernel later concatenates the lanes.
+// signed order-0 Exp-Golomb code of the int16 value in the low half of x (ExpGolomb.c:32-64):
+// v <= 0 -> 1 - 2v, v > 0 -> 2v; width = 2 * bit_length(code) - 1
+__device__ __forceinline__ uint32_t eg_code16(uint32_t x, uint32_t& width) {
+    const int32_t v = (int32_t)(int16_t)(uint16_t)x;
+    const uint32_t ng = (uint32_t)(-v);
+    const uint32_t code = ((ng << 1) ^ (uint32_t)((int32_t)ng >> 31)) + 1u;
+    width = 63u - 2u * (uint32_t)__clz((int)code);
+    return code;
+}
+
 template <int D>
 __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, EgFusedParams E) {
     constexpr int CS = 64 * D;
@@ -619,12 +629,15 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
         }
     }
 
-    // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp; a 64-bit
-    // accumulator, one MSB-first word out whenever 32 bits are pending (width <= 27 + 31 pending)
+    // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp, read from the
+    // staged cube, with a 64-bit accumulator: one MSB-first word out whenever 32 bits are pending
+    // (width <= 27, + 31 pending), word i of lane l at slot row i (i*64 + l).  eg_compact_kernel
+    // concatenates the lanes.  (Buffering the words in LDS first needs the values in registers to
+    // free the region: +6 % kernel time for the pack / unpack, more than the scattered stores cost.)
     const int cp = lane >> 3, part = lane & 7;
     const bool lvalid = cube0 + cp < P.n_cubes;
     const char* cb = wl + cp * CUBE_B;
-    uint32_t* dst = E.slot + (size_t)wid * E.lcap * 64 + lane;
+    uint32_t* dst = E.slot + (size_t)wid * E.seg_cap + lane;
     uint64_t acc = 0;
     uint32_t nb = 0, nw = 0;
     if (lvalid) {
@@ -632,14 +645,13 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
         for (int i0 = 0; i0 < VPL; i0 += 8) {
             const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
             const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
-            int v[8];
+            uint32_t v[8];
 #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = *(const int16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
+            for (int e = 0; e < 8; e++) v[e] = *(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                const uint32_t ng = (uint32_t)(-v[e]);
-                const uint32_t code = ((ng << 1) ^ (uint32_t)((int32_t)ng >> 31)) + 1u;  // v<=0: 1-2v, v>0: 2v
-                const uint32_t width = 63u - 2u * (uint32_t)__clz((int)code);
+                uint32_t width;
+                const uint32_t code = eg_code16(v[e], width);
                 acc = (acc << width) | code;
                 nb += width;
                 if (nb >= 32u) {

@@ -68,7 +68,7 @@ struct dct3d_ctx {
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
-    // fused encode + Exp-Golomb: per-segment lane slots and lane bit counts
+    // fused encode + Exp-Golomb: per-segment slots and lane bit counts
     DevBuf d_egf_slot, d_egf_lbits;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster;
@@ -595,8 +595,9 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (!d_out) return DCT3D_EINVAL;
     const int D = c->bd;
     const uint64_t n_seg = (n_cubes + 7) / 8, n_chunks = (n_seg + 4095) / 4096;
-    const uint32_t lcap = (uint32_t)((c->plan.cs / 8) * 27 + 31) / 32;  // cs/8 values x <= 27 bits
-    if ((rc = c->d_egf_slot.grow(n_seg * lcap * 64 * sizeof(uint32_t))) ||
+    // worst case per lane: cs/8 values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 14 bits)
+    const uint32_t seg_cap = (uint32_t)(64 * (((c->plan.cs / 8) * 27 + 31) / 32));
+    if ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
         (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
         (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
         (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
@@ -624,7 +625,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     E.group_of = (const uint8_t*)c->d_group_of.p;
     E.diag = (const uint16_t*)c->d_diag.p;
     E.slot = (uint32_t*)c->d_egf_slot.p;
-    E.lcap = lcap;
+    E.seg_cap = seg_cap;
     E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
     E.seg_bits = (uint32_t*)c->d_eg_bits.p;
     hipEvent_t* ev = timing_slot(c);
@@ -646,7 +647,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     G.carry_bits = (uint32_t)carry_bits;
     G.carry_byte = carry_byte;
     if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_eg_compact(D, G, E.slot, E.lane_bits, lcap, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     uint64_t st[2] = {0, 0};
     if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
