@@ -327,33 +327,59 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 //                 starts at the true first bit, so by induction every start is then a true boundary.
 //                 Exp-Golomb parses resynchronise within a few codewords, so two passes are typical.
 //   scan          value index of each chunk's first codeword
-//   write pass    each chunk parsed once more from its (true) start; value idx goes to cube idx / cs,
-//                 diagonal position idx % cs; the end bit of value n_values - 1 is recorded.
+//   mark pass     each chunk parsed once more from its (true) start: the bit position of every 32nd
+//                 value goes to mark[idx / 32]; the end bit of value n_values - 1 is recorded
+//   emit          one wave per 2,048 values (4 cubes of 8x8x8 / 8 of 8x8x4): lane l parses the 32
+//                 values from mark[l]; the wave scatters them to their diagonal positions in LDS and
+//                 writes the cubes with 1 KiB coalesced stores
+// The parses read the stream from LDS: the block (sync, mark) or the wave (emit) first stages its
+// contiguous bit range with coalesced loads.  (A parse reading global memory waits a full memory
+// round trip at nearly every code: some lane of the wave refills on ~94 % of the codes, and the
+// wave-wide vmcnt cannot wait for one lane's word only.  A per-value scatter of the values to their
+// cubes -- 2.1 G single-dword stores per 128 stacks -- took 47 ms.)
 // A parse that meets 32 zero bits (no valid code has more than 30 leading zeros) ends "invalid":
 // in a true parse inside the wanted values that means a corrupt stream.
 constexpr uint64_t kChunkBits = 1024;
 constexpr uint64_t kNoExit = ~0ull;
+// a block's window: its 256 chunks plus slack (a parse ends < 27 bits past its chunk; the reader's
+// buffer and the long-code path look < 96 bits ahead of its position)
+constexpr uint32_t kSyncWinWords = kEgBlock * (uint32_t)(kChunkBits / 32) + 8;
+constexpr uint32_t kMarkVals = 32;          // values per emit lane / per mark
+constexpr uint32_t kEmitWinWords = 2048;    // per wave: window (<= 2,048 values x 27 bits) / 8 KiB staging
+
+// stream words [w0, w0 + n), byte-swapped to MSB-first, in LDS; zero outside (past the end of the
+// data -- and, on a corrupt stream only, past the window)
+struct LdsBits {
+    const uint32_t* s;
+    uint64_t w0;
+    uint32_t n;
+    __device__ __forceinline__ uint32_t word(uint64_t k) const {
+        const uint64_t i = k - w0;
+        return i < n ? s[i] : 0u;
+    }
+};
+__device__ __forceinline__ uint32_t stream_word(const EgDecParams& P, uint64_t k) {
+    return k < P.n_words ? __builtin_bswap32(P.words[k]) : 0u;
+}
 
 struct BitReader {
-    const uint32_t* w;
-    uint64_t nw;
+    LdsBits L;
     uint64_t next;   // next word to load
     uint64_t buf;    // left-aligned bits [pos, pos + avail)
     int avail;
     uint64_t pos;
-    __device__ __forceinline__ uint32_t word(uint64_t k) const { return k < nw ? __builtin_bswap32(w[k]) : 0u; }
     __device__ __forceinline__ void seek(uint64_t p) {
         pos = p;
         const uint64_t k = p >> 5;
         const int sh = (int)(p & 31);
-        buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+        buf = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
         avail = 64 - sh;
         next = k + 2;
     }
     // one codeword: false when 32 zero bits come first (invalid); *code = the (z+1)-bit value
     __device__ __forceinline__ bool get(uint32_t& code) {
         if (avail <= 32) {
-            buf |= (uint64_t)word(next++) << (32 - avail);
+            buf |= (uint64_t)L.word(next++) << (32 - avail);
             avail += 32;
         }
         const int z = buf ? __clzll((long long)buf) : 64;
@@ -367,8 +393,8 @@ struct BitReader {
         } else {  // a long code straddling the buffer: read it at its absolute position
             const uint64_t k = pos >> 5;
             const int sh = (int)(pos & 31);
-            const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
-            const uint64_t win = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
+            const uint64_t hi = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
+            const uint64_t win = sh ? (hi | ((uint64_t)L.word(k + 2) >> (32 - sh))) : hi;
             code = (uint32_t)(win >> (64 - width));
             seek(pos + (uint64_t)width);
         }
@@ -388,11 +414,21 @@ __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t
     return e == kNoExit ? P.start_bit + t * kChunkBits : e;
 }
 
+// the block's window: chunks [blockIdx.x * kEgBlock, +kEgBlock), coalesced, then a barrier
+__device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win) {
+    const uint64_t w0 = (P.start_bit + (uint64_t)blockIdx.x * kEgBlock * kChunkBits) >> 5;
+    for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += kEgBlock) win[i] = stream_word(P, w0 + i);
+    __syncthreads();
+    return LdsBits{win, w0, kSyncWinWords};
+}
+
 __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration) {
+    __shared__ uint32_t win[kSyncWinWords];
+    const LdsBits L = stage_block_window(P, win);
     const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (t >= P.n_chunks) return;
     const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
-    BitReader r{P.words, P.n_words, 0, 0, 0, 0};
+    BitReader r{L, 0, 0, 0, 0};
     r.seek(chunk_start(P, t, iteration));
     uint32_t n = 0, code;
     bool invalid = false;
@@ -409,18 +445,18 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     if (iteration > 0 && ex != P.exit_in[t]) atomicOr((unsigned int*)&P.status[0], 1u);
 }
 
-__global__ __launch_bounds__(kEgBlock) void eg_decode_write_kernel(EgDecParams P) {
+__global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
+    __shared__ uint32_t win[kSyncWinWords];
+    const LdsBits L = stage_block_window(P, win);
     const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (t >= P.n_chunks) return;
     uint64_t idx = P.off[t];
     if (idx >= P.n_values) return;
     const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
-    BitReader r{P.words, P.n_words, 0, 0, 0, 0};
     // the converged exits are in exit_in (the host swaps the buffers after every pass)
     const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
-    if (s == kNoExit) {  // the true parse stopped in an earlier chunk: reported by that chunk
-        return;
-    }
+    if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
+    BitReader r{L, 0, 0, 0, 0};
     r.seek(s);
     uint32_t code;
     while (idx < P.n_values && r.pos < end) {
@@ -430,9 +466,63 @@ __global__ __launch_bounds__(kEgBlock) void eg_decode_write_kernel(EgDecParams P
             atomicOr((unsigned int*)&P.status[2], p0 + 32 <= P.limit_bit && r.pos <= P.limit_bit ? 1u : 2u);
             return;
         }
-        const uint64_t cube = idx / (uint64_t)P.cs;
-        P.q[cube * P.cs + P.diag[idx - cube * P.cs]] = eg_value(code);
+        if ((idx & (kMarkVals - 1)) == 0) P.mark[idx / kMarkVals] = p0;
         if (++idx == P.n_values) P.status[1] = r.pos;  // the bit after the last wanted value
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
+    constexpr uint32_t CS = 64 * D, PARTS = CS / kMarkVals, CPW = 64 / PARTS;
+    static_assert(CPW * CS * 4 == kEmitWinWords * 4, "one wave's cubes fill its staging");
+    __shared__ uint32_t lds[kEgWaves][kEmitWinWords];
+    __shared__ uint16_t s_diag[CS];
+    if (P.status[2] != 0) return;  // corrupt / short stream: reported, nothing written (block-uniform)
+    for (uint32_t i = threadIdx.x; i < CS; i += kEgBlock) s_diag[i] = P.diag[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t n_marks = P.n_values / kMarkVals;
+    const uint64_t m0 = ((uint64_t)blockIdx.x * kEgWaves + wave) * 64;
+    if (m0 >= n_marks) return;
+    const bool lv = m0 + lane < n_marks;
+    const uint64_t my = lv ? P.mark[m0 + lane] : 0;
+    const uint64_t first = __shfl(my, 0, 64);
+    const uint64_t last = m0 + 64 < n_marks ? P.mark[m0 + 64] : P.status[1];  // wave-uniform
+    const uint64_t w0 = first >> 5;
+    const uint64_t span = (last >> 5) + 4 - w0;
+    const uint32_t nwin = (uint32_t)(span < kEmitWinWords ? span : kEmitWinWords);  // bounded on any input
+    uint32_t* wl = lds[wave];
+    for (uint32_t i = lane; i < nwin; i += 64) wl[i] = stream_word(P, w0 + i);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int32_t v[kMarkVals];
+    {
+        BitReader r{LdsBits{wl, w0, nwin}, 0, 0, 0, 0};
+        r.seek(my);
+#pragma unroll
+        for (uint32_t i = 0; i < kMarkVals; i++) {
+            uint32_t code = 1u;
+            (void)r.get(code);  // the mark pass has validated the stream
+            v[i] = eg_value(code);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t c = lane / PARTS, part = lane % PARTS;
+    int32_t* st = (int32_t*)wl + c * CS;
+#pragma unroll
+    for (uint32_t i = 0; i < kMarkVals; i++) st[s_diag[part * kMarkVals + i]] = v[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int32_t* q = P.q + m0 * kMarkVals;  // value index of the wave's first cube
+    const uint64_t nv = P.n_values - m0 * kMarkVals;
+#pragma unroll
+    for (uint32_t t = 0; t < 8; t++) {
+        const uint32_t e = (t * 64 + lane) * 4;
+        if (e < nv) *(int4*)(q + e) = *(const int4*)((const int32_t*)wl + e);
     }
 }
 
@@ -491,10 +581,13 @@ int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* l
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_decode_write(const EgDecParams& P, hipStream_t st) {
+int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st) {
     if (P.n_chunks == 0) return 0;
-    hipLaunchKernelGGL(eg_decode_write_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock),
-                       0, st, P);
+    hipLaunchKernelGGL(eg_mark_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+    const uint64_t waves = (P.n_values / kMarkVals + 63) / 64;
+    const uint32_t blocks = (uint32_t)((waves + kEgWaves - 1) / kEgWaves);
+    if (D == 8) hipLaunchKernelGGL(eg_emit_kernel<8>, dim3(blocks), dim3(kEgBlock), 0, st, P);
+    else hipLaunchKernelGGL(eg_emit_kernel<4>, dim3(blocks), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -107,6 +107,7 @@ struct EgDecParams {
     uint32_t* count;           // codewords per chunk
     uint64_t* off;             // value index of each chunk's first codeword (scan)
     uint64_t* status;          // [0] changed / first invalid chunk, [1] end bit, [2] flags 1 corrupt, [3] values
+    uint64_t* mark;            // [n_values / 32] bit position of every 32nd value
     int32_t* q;                // cube-major output
 };
 
@@ -135,7 +136,7 @@ int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* l
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st);
 int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
-int launch_eg_decode_write(const EgDecParams& P, hipStream_t st);
+int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mark pass + emit
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
 int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
 int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,

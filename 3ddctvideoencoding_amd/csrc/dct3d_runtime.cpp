@@ -71,7 +71,7 @@ struct dct3d_ctx {
     // fused encode + Exp-Golomb: per-segment slots and lane bit counts
     DevBuf d_egf_slot, d_egf_lbits;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
-    DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster;
+    DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
     uint64_t eg_last_bytes = 0;
 };
 
@@ -733,6 +733,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (!rc) rc = c->d_eg_bits.grow(n_chunks * sizeof(uint32_t));
     if (!rc) rc = c->d_eg_off.grow(n_chunks * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
+    if (!rc) rc = c->d_egd_mark.grow((n_cubes * (uint64_t)c->plan.cs / 32 + 1) * sizeof(uint64_t));
     if (rc) return rc;
     EgDecParams D;
     D.words = (const uint32_t*)d_bytes;
@@ -747,6 +748,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     D.count = (uint32_t*)c->d_eg_bits.p;
     D.off = (uint64_t*)c->d_eg_off.p;
     D.status = (uint64_t*)c->d_egd_status.p;
+    D.mark = (uint64_t*)c->d_egd_mark.p;
     D.q = d_q;
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts; two passes
     // are the usual total); at most n_chunks + 1 passes by induction from chunk 0
@@ -777,7 +779,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
-    if (launch_eg_decode_write(D, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_decode_write(c->bd, D, c->stream)) return DCT3D_EKERNEL;
     uint64_t st[4] = {0, 0, 0, 0}, total[2] = {0, 0};
     if (hipMemcpyAsync(st, c->d_egd_status.p, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipMemcpyAsync(total, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||

@@ -36,6 +36,8 @@ CONFIGS = {
     "c6_decode_1080p_d4": (1920, 1080, 4, 128, "decode"),
     # encode to the Exp-Golomb stream: DCT + quantise + diagonal order + EG per step
     "c7_encode_eg_1080p": (1920, 1080, 8, 128, "encode_eg"),
+    # decode from the Exp-Golomb stream: EG decode + dequantise + IDCT per step
+    "c8_decode_eg_1080p": (1920, 1080, 8, 128, "decode_eg"),
 }
 
 
@@ -167,6 +169,21 @@ def main():
 
         def step():
             ctx.decode_stacks_dev(q, width, height, stacks, out)
+    elif direction == "decode_eg":
+        eg_cap = n_cubes * cs
+        eg_stream = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
+        eg_info["bits"] = ctx.encode_eg_dev(frames, width, height, stacks, eg_stream, eg_cap)  # the encoder's stream
+        nbytes = (eg_info["bits"] + 7) // 8
+        out = torch.empty_like(frames)
+        eg_ev = []
+
+        def step():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ctx.eg_decode_dev(eg_stream, nbytes, 0, n_cubes, q)  # synchronises (status read back)
+            e1.record()
+            eg_ev.append((e0, e1))
+            ctx.decode_stacks_dev(q, width, height, stacks, out)
     elif direction == "encode_eg" and a.eg_two_step:
         eg_cap = n_cubes * cs  # 8 bits per value: far above what quantised content needs
         eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
@@ -223,7 +240,7 @@ def main():
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
     fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
     achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
-    kname = "decode_kernel" if direction == "decode" else ("encode_eg_kernel" if fused else "encode_kernel")
+    kname = "decode_kernel" if direction in ("decode", "decode_eg") else ("encode_eg_kernel" if fused else "encode_kernel")
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
@@ -237,11 +254,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64" if direction == "decode" else "f32",
+        "dtype": "f64" if direction in ("decode", "decode_eg") else "f32",
         "data": "synthetic",
         "config": {
             "workload": f"{width}x{height} grayscale, {depth}-frame stacks, "
-                        f"{ {'encode': 'forward 3D DCT + quantise', 'decode': 'dequantise + inverse 3D DCT', 'encode_eg': 'forward 3D DCT + quantise + diagonal order + Exp-Golomb stream'}[direction] }"
+                        f"{ {'encode': 'forward 3D DCT + quantise', 'decode': 'dequantise + inverse 3D DCT', 'encode_eg': 'forward 3D DCT + quantise + diagonal order + Exp-Golomb stream', 'decode_eg': 'Exp-Golomb decode + dequantise + inverse 3D DCT'}[direction] }"
                         f" ({unit_name} cubes), {stacks} device-resident stacks per GPU per step",
             "name": a.config,
             "stacks_per_gpu": stacks,
@@ -267,8 +284,8 @@ def main():
         "flagged_units_last_step": st["n_flagged"],
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,
-        "eg_stage": None if direction != "encode_eg" else {
-            "path": "fused" if fused else "two-step",
+        "eg_stage": None if direction not in ("encode_eg", "decode_eg") else {
+            "path": "decode" if direction == "decode_eg" else ("fused" if fused else "two-step"),
             "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
             "bits_per_value": eg_info["bits"] / (n_cubes * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
