@@ -37,7 +37,7 @@ ABI_SYMBOLS = (
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
     "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev",
     "dct3d_eg_encode_dev", "dct3d_encode_eg", "dct3d_eg_fetch", "dct3d_diagonal_order",
-    "dct3d_eg_decode_dev", "dct3d_decode_eg", "dct3d_encode_eg_dev",
+    "dct3d_eg_decode_dev", "dct3d_decode_eg", "dct3d_encode_eg_dev", "dct3d_decode_eg_dev",
 )
 
 
@@ -106,6 +106,7 @@ def lib() -> C.CDLL:
         L.dct3d_diagonal_order.argtypes = [i32, i32, i32, vp]
         L.dct3d_eg_decode_dev.argtypes = [vp, vp, u64, u64, u64, vp, C.POINTER(u64)]
         L.dct3d_decode_eg.argtypes = [vp, vp, u64, i32, i32, i32, i32, vp, C.POINTER(u64)]
+        L.dct3d_decode_eg_dev.argtypes = [vp, vp, u64, u64, i32, i32, i32, vp, C.POINTER(u64)]
         _lib = L
     return _lib
 
@@ -314,6 +315,15 @@ class Context:
         eb = C.c_uint64(0)
         _check(lib().dct3d_eg_decode_dev(self._h, _tptr(d_bytes), nbytes, start_bit, n_cubes, _tptr(d_q), C.byref(eb)),
                "dct3d_eg_decode_dev")
+        return eb.value
+
+    def decode_eg_dev(self, d_bytes, nbytes: int, start_bit: int, width: int, height: int, n_stacks: int,
+                      d_frames) -> int:
+        """Fused device path: Exp-Golomb stream (device, 4-byte aligned) -> u8 frames (device), no int32
+        intermediate; returns the bit after the last value."""
+        eb = C.c_uint64(0)
+        _check(lib().dct3d_decode_eg_dev(self._h, _tptr(d_bytes), nbytes, start_bit, width, height, n_stacks,
+                                         _tptr(d_frames), C.byref(eb)), "dct3d_decode_eg_dev")
         return eb.value
 
     def decode_eg(self, stream: bytes, width: int, height: int, n_stacks: int, start_bit: int = 0):

@@ -18,6 +18,7 @@
 
 #include <cstdint>
 
+#include "dct3d_eg_bits.h"
 #include "dct3d_kernels.h"
 
 namespace dct3d {
@@ -339,73 +340,13 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 // cubes -- 2.1 G single-dword stores per 128 stacks -- took 47 ms.)
 // A parse that meets 32 zero bits (no valid code has more than 30 leading zeros) ends "invalid":
 // in a true parse inside the wanted values that means a corrupt stream.
-constexpr uint64_t kChunkBits = 1024;
+constexpr uint64_t kChunkBits = kEgChunkBits;
 constexpr uint64_t kNoExit = ~0ull;
 // a block's window: its 256 chunks plus slack (a parse ends < 27 bits past its chunk; the reader's
 // buffer and the long-code path look < 96 bits ahead of its position)
 constexpr uint32_t kSyncWinWords = kEgBlock * (uint32_t)(kChunkBits / 32) + 8;
 constexpr uint32_t kMarkVals = 32;          // values per emit lane / per mark
 constexpr uint32_t kEmitWinWords = 2048;    // per wave: window (<= 2,048 values x 27 bits) / 8 KiB staging
-
-// stream words [w0, w0 + n), byte-swapped to MSB-first, in LDS; zero outside (past the end of the
-// data -- and, on a corrupt stream only, past the window)
-struct LdsBits {
-    const uint32_t* s;
-    uint64_t w0;
-    uint32_t n;
-    __device__ __forceinline__ uint32_t word(uint64_t k) const {
-        const uint64_t i = k - w0;
-        return i < n ? s[i] : 0u;
-    }
-};
-__device__ __forceinline__ uint32_t stream_word(const EgDecParams& P, uint64_t k) {
-    return k < P.n_words ? __builtin_bswap32(P.words[k]) : 0u;
-}
-
-struct BitReader {
-    LdsBits L;
-    uint64_t next;   // next word to load
-    uint64_t buf;    // left-aligned bits [pos, pos + avail)
-    int avail;
-    uint64_t pos;
-    __device__ __forceinline__ void seek(uint64_t p) {
-        pos = p;
-        const uint64_t k = p >> 5;
-        const int sh = (int)(p & 31);
-        buf = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
-        avail = 64 - sh;
-        next = k + 2;
-    }
-    // one codeword: false when 32 zero bits come first (invalid); *code = the (z+1)-bit value
-    __device__ __forceinline__ bool get(uint32_t& code) {
-        if (avail <= 32) {
-            buf |= (uint64_t)L.word(next++) << (32 - avail);
-            avail += 32;
-        }
-        const int z = buf ? __clzll((long long)buf) : 64;
-        if (z >= 32) return false;
-        const int width = 2 * z + 1;
-        if (width <= avail) {
-            code = (uint32_t)(buf >> (64 - width));
-            buf <<= width;
-            avail -= width;
-            pos += (uint64_t)width;
-        } else {  // a long code straddling the buffer: read it at its absolute position
-            const uint64_t k = pos >> 5;
-            const int sh = (int)(pos & 31);
-            const uint64_t hi = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
-            const uint64_t win = sh ? (hi | ((uint64_t)L.word(k + 2) >> (32 - sh))) : hi;
-            code = (uint32_t)(win >> (64 - width));
-            seek(pos + (uint64_t)width);
-        }
-        return true;
-    }
-};
-
-__device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader.java:52-62
-    const uint32_t m = code - 1u;
-    return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
-}
 
 __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t, int iteration) {
     if (t == 0) return P.start_bit;
@@ -422,24 +363,37 @@ __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint
     return LdsBits{win, w0, kSyncWinWords};
 }
 
+// window-relative form of an absolute bit position (clamped: positions past the window behave as the
+// window's end, which only a limit or end beyond the window ever is)
+__device__ __forceinline__ uint32_t rel_bit(uint64_t p, uint64_t base) {
+    return p <= base ? 0u : (p - base >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(p - base));
+}
+
 __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration) {
     __shared__ uint32_t win[kSyncWinWords];
     const LdsBits L = stage_block_window(P, win);
     const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (t >= P.n_chunks) return;
-    const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
-    BitReader r{L, 0, 0, 0, 0};
-    r.seek(chunk_start(P, t, iteration));
+    const uint64_t base = L.w0 * 32;
+    const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
+    const uint32_t limit = rel_bit(P.limit_bit, base);
+    const uint32_t stop = min(end, limit);
+    WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
+    r.seek(rel_bit(chunk_start(P, t, iteration), base));
     uint32_t n = 0, code;
     bool invalid = false;
-    while (r.pos < end && r.pos < P.limit_bit) {
-        if (!r.get(code) || r.pos > P.limit_bit) {  // 32 zero bits, or a code running past the data
+    // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary
+    while (r.pos < stop) {
+        n += r.ones(min(stop - r.pos, 64u));
+        if (r.pos >= stop) break;
+        if (!r.at_long_code()) continue;  // the buffered bits ran out inside the run: refill
+        if (!r.get(code) || r.pos > limit) {  // 32 zero bits, or a code running past the data
             invalid = true;
             break;
         }
         n++;
     }
-    const uint64_t ex = invalid ? kNoExit : r.pos;
+    const uint64_t ex = invalid ? kNoExit : base + r.pos;
     P.exit_out[t] = ex;
     P.count[t] = n;
     if (iteration > 0 && ex != P.exit_in[t]) atomicOr((unsigned int*)&P.status[0], 1u);
@@ -452,22 +406,38 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     if (t >= P.n_chunks) return;
     uint64_t idx = P.off[t];
     if (idx >= P.n_values) return;
-    const uint64_t end = P.start_bit + (t + 1) * kChunkBits;
     // the converged exits are in exit_in (the host swaps the buffers after every pass)
     const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
     if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
-    BitReader r{L, 0, 0, 0, 0};
-    r.seek(s);
+    const uint64_t base = L.w0 * 32;
+    const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
+    const uint32_t limit = rel_bit(P.limit_bit, base);
+    WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
+    r.seek(rel_bit(s, base));
     uint32_t code;
     while (idx < P.n_values && r.pos < end) {
-        const uint64_t p0 = r.pos;
-        if (p0 >= P.limit_bit || !r.get(code) || r.pos > P.limit_bit) {
-            // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
-            atomicOr((unsigned int*)&P.status[2], p0 + 32 <= P.limit_bit && r.pos <= P.limit_bit ? 1u : 2u);
+        const uint32_t p0 = r.pos;
+        if (p0 >= limit) {  // ran out of bits
+            atomicOr((unsigned int*)&P.status[2], 2u);
             return;
         }
-        if ((idx & (kMarkVals - 1)) == 0) P.mark[idx / kMarkVals] = p0;
-        if (++idx == P.n_values) P.status[1] = r.pos;  // the bit after the last wanted value
+        const uint64_t room = min((uint64_t)min(end - p0, limit - p0), P.n_values - idx);
+        const uint32_t k = r.ones((uint32_t)min(room, (uint64_t)64));
+        if (k) {  // values idx .. idx + k - 1 are zeros at bits p0 .. p0 + k - 1
+            for (uint64_t m = (idx + kMarkVals - 1) & ~(uint64_t)(kMarkVals - 1); m < idx + k; m += kMarkVals)
+                P.mark[m / kMarkVals] = base + p0 + (m - idx);
+            idx += k;
+            if (idx == P.n_values) P.status[1] = base + r.pos;  // the bit after the last wanted value
+            continue;
+        }
+        if (!r.at_long_code()) continue;  // refill
+        if (!r.get(code) || r.pos > limit) {
+            // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
+            atomicOr((unsigned int*)&P.status[2], (uint64_t)p0 + 32 <= limit && r.pos <= limit ? 1u : 2u);
+            return;
+        }
+        if ((idx & (kMarkVals - 1)) == 0) P.mark[idx / kMarkVals] = base + p0;
+        if (++idx == P.n_values) P.status[1] = base + r.pos;
     }
 }
 
@@ -498,8 +468,8 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int32_t v[kMarkVals];
     {
-        BitReader r{LdsBits{wl, w0, nwin}, 0, 0, 0, 0};
-        r.seek(my);
+        WinReader r{wl, nwin, 0, 0, 0, 0, 0};
+        r.seek(rel_bit(my, w0 * 32));
 #pragma unroll
         for (uint32_t i = 0; i < kMarkVals; i++) {
             uint32_t code = 1u;
@@ -581,14 +551,24 @@ int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* l
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st) {
+int launch_eg_mark(const EgDecParams& P, hipStream_t st) {
     if (P.n_chunks == 0) return 0;
     hipLaunchKernelGGL(eg_mark_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st) {
     const uint64_t waves = (P.n_values / kMarkVals + 63) / 64;
+    if (waves == 0) return 0;
     const uint32_t blocks = (uint32_t)((waves + kEgWaves - 1) / kEgWaves);
     if (D == 8) hipLaunchKernelGGL(eg_emit_kernel<8>, dim3(blocks), dim3(kEgBlock), 0, st, P);
     else hipLaunchKernelGGL(eg_emit_kernel<4>, dim3(blocks), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st) {
+    if (launch_eg_mark(P, st)) return -1;
+    return launch_eg_emit(D, P, st);
 }
 
 }  // namespace dct3d

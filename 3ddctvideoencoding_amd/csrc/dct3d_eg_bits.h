@@ -1,0 +1,169 @@
+// dct3d_eg_bits.h -- Exp-Golomb bit reading on the device, shared by the stream decoder
+// (dct3d_eg.hip) and the fused stream -> raster decode (dct3d_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dct3d_kernels.h"
+
+namespace dct3d {
+
+// stream words [w0, w0 + n), byte-swapped to MSB-first, in LDS; zero outside (past the end of the
+// data -- and, on a corrupt stream only, past the window)
+struct LdsBits {
+    const uint32_t* s;
+    uint64_t w0;
+    uint32_t n;
+    __device__ __forceinline__ uint32_t word(uint64_t k) const {
+        const uint64_t i = k - w0;
+        const uint32_t v = s[i < n ? i : 0];  // unconditional read (a read under a branch is waited at the join)
+        return i < n ? v : 0u;
+    }
+};
+// the stream in global memory (the decode fixup's re-parse of a replayed cube: rare, latency-bound)
+struct GlobalBits {
+    const uint32_t* w;
+    uint64_t nw;
+    __device__ __forceinline__ uint32_t word(uint64_t k) const {
+        const uint32_t v = w[k < nw ? k : nw - 1];
+        return k < nw ? __builtin_bswap32(v) : 0u;
+    }
+};
+__device__ __forceinline__ uint32_t stream_word(const EgDecParams& P, uint64_t k) {
+    return k < P.n_words ? __builtin_bswap32(P.words[k]) : 0u;
+}
+
+template <class Src>
+struct BitReader {
+    Src L;
+    uint64_t next;   // index of the word held in `pre`
+    uint64_t buf;    // left-aligned bits [pos, pos + avail)
+    int avail;
+    uint64_t pos;
+    uint32_t pre;    // word `next`, read one refill ahead: some lane of the wave refills on almost every
+                     // code, so a read on demand put its full latency on every code
+    __device__ __forceinline__ void seek(uint64_t p) {
+        pos = p;
+        const uint64_t k = p >> 5;
+        const int sh = (int)(p & 31);
+        buf = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
+        avail = 64 - sh;
+        next = k + 2;
+        pre = L.word(next);
+    }
+    __device__ __forceinline__ void refill() {
+        if (avail <= 32) {
+            buf |= (uint64_t)pre << (32 - avail);
+            avail += 32;
+            pre = L.word(++next);
+        }
+    }
+    // A run of 1-bit codes (value 0, the common case: ~80 % of the codes of quantised content):
+    // consumes up to maxn of them at once (clz of the complement); returns how many.  The run stops at
+    // a 0 bit (a longer code starts), at maxn, or where the buffered bits end (call again).
+    __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
+        refill();
+        const uint64_t inv = ~buf;
+        uint32_t n1 = inv ? (uint32_t)__clzll((long long)inv) : 64u;
+        n1 = min(min(n1, (uint32_t)avail), maxn);
+        buf = n1 >= 64 ? 0ull : buf << n1;
+        avail -= (int)n1;
+        pos += n1;
+        return n1;
+    }
+    // the next buffered bit is 0 (a code longer than one bit starts here)
+    __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
+    // one codeword: false when 32 zero bits come first (invalid); *code = the (z+1)-bit value
+    __device__ __forceinline__ bool get(uint32_t& code) {
+        refill();
+        const int z = buf ? __clzll((long long)buf) : 64;
+        if (z >= 32) return false;
+        const int width = 2 * z + 1;
+        if (width <= avail) {
+            code = (uint32_t)(buf >> (64 - width));
+            buf <<= width;
+            avail -= width;
+            pos += (uint64_t)width;
+        } else {  // a long code straddling the buffer: read it at its absolute position
+            const uint64_t k = pos >> 5;
+            const int sh = (int)(pos & 31);
+            const uint64_t hi = (((uint64_t)L.word(k) << 32) | L.word(k + 1)) << sh;
+            const uint64_t win = sh ? (hi | ((uint64_t)L.word(k + 2) >> (32 - sh))) : hi;
+            code = (uint32_t)(win >> (64 - width));
+            seek(pos + (uint64_t)width);
+        }
+        return true;
+    }
+};
+
+// The same reader over an LDS window with window-relative 32-bit positions (a window holds < 2^18
+// bits): the per-code 64-bit index, compare and carry arithmetic of absolute positions was most of the
+// parse's instructions.  Word i of the window is s[i] (i < n), zero beyond.
+struct WinReader {
+    const uint32_t* s;
+    uint32_t n;
+    uint32_t next;   // index of the word held in `pre`
+    uint64_t buf;    // left-aligned bits [pos, pos + avail)
+    int avail;
+    uint32_t pos;
+    uint32_t pre;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+        const uint32_t v = s[i < n ? i : 0u];  // unconditional read
+        return i < n ? v : 0u;
+    }
+    __device__ __forceinline__ void seek(uint32_t p) {
+        pos = p;
+        const uint32_t k = p >> 5;
+        const int sh = (int)(p & 31);
+        buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+        avail = 64 - sh;
+        next = k + 2;
+        pre = word(next);
+    }
+    __device__ __forceinline__ void refill() {
+        if (avail <= 32) {
+            buf |= (uint64_t)pre << (32 - avail);
+            avail += 32;
+            pre = word(++next);
+        }
+    }
+    __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
+        refill();
+        const uint64_t inv = ~buf;
+        uint32_t n1 = inv ? (uint32_t)__clzll((long long)inv) : 64u;
+        n1 = min(min(n1, (uint32_t)avail), maxn);
+        buf = n1 >= 64 ? 0ull : buf << n1;
+        avail -= (int)n1;
+        pos += n1;
+        return n1;
+    }
+    __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
+    __device__ __forceinline__ bool get(uint32_t& code) {
+        refill();
+        const int z = buf ? __clzll((long long)buf) : 64;
+        if (z >= 32) return false;
+        const int width = 2 * z + 1;
+        if (width <= avail) {
+            code = (uint32_t)(buf >> (64 - width));
+            buf <<= width;
+            avail -= width;
+            pos += (uint32_t)width;
+        } else {  // a long code straddling the buffer (|v| >= 2^16: never for quantised 8-bit content)
+            const uint32_t k = pos >> 5;
+            const int sh = (int)(pos & 31);
+            const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+            const uint64_t w = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
+            code = (uint32_t)(w >> (64 - width));
+            seek(pos + (uint32_t)width);
+        }
+        return true;
+    }
+};
+
+__device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader.java:52-62
+    const uint32_t m = code - 1u;
+    return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
+}
+
+}  // namespace dct3d

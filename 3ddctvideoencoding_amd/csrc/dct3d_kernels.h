@@ -65,6 +65,11 @@ struct DecodeFixupParams {
     uint32_t flag_cap;
     const uint32_t* cube_list;
     const double* inv_coef_t;  // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
+    // in == nullptr (fused stream decode): a replayed cube's values are re-parsed from the stream
+    const uint32_t* words;
+    uint64_t n_words;
+    const uint64_t* mark;      // bit position of every 32nd value (EgDecParams::mark)
+    const uint16_t* diag;
 };
 
 struct Fwd64Params {
@@ -94,6 +99,7 @@ struct EgParams {
 };
 
 // Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)
+constexpr uint64_t kEgChunkBits = 512;  // bits per parse chunk (one thread each)
 struct EgDecParams {
     const uint32_t* words;     // stream, memory byte order
     uint64_t n_words;
@@ -137,6 +143,10 @@ int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st);
 int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
 int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mark pass + emit
+int launch_eg_mark(const EgDecParams& P, hipStream_t st);
+int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st);
+// fused stream -> raster decode: values parsed at the marks straight into the decode's LDS staging
+int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st);
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
 int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
 int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,

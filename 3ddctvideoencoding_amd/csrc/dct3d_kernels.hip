@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "dct_butterfly.h"
+#include "dct3d_eg_bits.h"
 #include "dct3d_kernels.h"
 
 namespace dct3d {
@@ -992,6 +993,64 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     decode_tile<D, PG>(P, wl, lane, cube0, [] {});
 }
 
+// Fused stream -> raster decode (dct3d_decode_eg_dev; decoder.c:209-295 after the inflate): the
+// wave's CPW cubes are the 2,048 consecutive stream values at marks m0 .. m0 + 63 (the stream decoder's
+// mark pass: bit position of every 32nd value).  The wave stages its bit range in its LDS region, lane
+// l parses the 32 values from mark m0 + l into registers, the region then receives them at their
+// diagonal positions in the decode's staging layout (face-padded cube-major), and decode_tile runs as
+// in decode_kernel.  No int32 cube-major array is written or read.
+template <int D>
+__global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, EgDecParams E) {
+    using G = DecGeom<D>;
+    constexpr uint32_t CS = G::CS, PARTS = CS / 32, CPW = G::CPW;
+    static_assert(CPW * CS == 2048 && PARTS * CPW == 64, "one wave = 64 marks");
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
+    __shared__ uint16_t s_diag[CS];
+    if (E.status[2] != 0) return;  // corrupt / short stream: reported by the mark pass (block-uniform)
+    for (uint32_t i = threadIdx.x; i < CS; i += kBlock) s_diag[i] = E.diag[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    char* wl = lds + wave * kDecWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * CPW;
+    if (cube0 >= P.n_cubes) return;
+    const uint64_t n_marks = E.n_values / 32;
+    const uint64_t m0 = (uint64_t)cube0 * CS / 32;
+    const bool lv = m0 + lane < n_marks;
+    const uint64_t my = lv ? E.mark[m0 + lane] : 0;
+    const uint64_t first = __shfl(my, 0, 64);
+    const uint64_t last = m0 + 64 < n_marks ? E.mark[m0 + 64] : E.status[1];  // wave-uniform
+    const uint64_t w0 = first >> 5;
+    const uint64_t span = (last >> 5) + 4 - w0;
+    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,304 words >= 2,048 values x 27 bits
+    const uint32_t nwin = (uint32_t)(span < WIN ? span : WIN);  // bounded on any input
+    uint32_t* win = (uint32_t*)wl;
+    for (uint32_t i = lane; i < nwin; i += 64) win[i] = stream_word(E, w0 + i);
+    wave_lds_sync();
+    int32_t v[32];
+    {
+        WinReader r{win, nwin, 0, 0, 0, 0, 0};
+        r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            uint32_t code = 1u;
+            (void)r.get(code);  // the mark pass has validated the stream
+            v[i] = eg_value(code);
+        }
+    }
+    wave_lds_sync();
+    {
+        const uint32_t c = lane / PARTS, part = lane % PARTS;
+        char* cb = wl + c * G::SA_C;
+#pragma unroll
+        for (int i = 0; i < 32; i++) {
+            const uint32_t k = s_diag[part * 32 + i];
+            *(int32_t*)(cb + (k >> 6) * G::SA_F + (k & 63) * 4) = v[i];
+        }
+    }
+    wave_lds_sync();
+    decode_tile<D, 1>(P, wl, lane, cube0, [] {});
+}
+
 // DIAGNOSTIC variants (DCT3D_DEC_VARIANT=7 / 8; the output is NOT a decode): MODE 1 = memory only
 // (the same loads, staging and raster stores, no transform), MODE 2 = compute only (no global loads;
 // stores suppressed by a runtime condition).  They split the kernel's time into its memory and compute
@@ -1074,9 +1133,21 @@ __global__ __launch_bounds__(256) void decode_fixup_kernel(DecodeFixupParams P) 
     for (uint32_t ci = blockIdx.x; ci < ncube; ci += gridDim.x) {
         const uint32_t g = P.cube_list[ci];
         __syncthreads();
-        for (int k = threadIdx.x; k < CS; k += blockDim.x) {
-            const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-            cf[k] = (double)P.in[(size_t)g * CS + k] * (double)max(1, 5 * (kx + ky + kz));
+        if (P.in) {
+            for (int k = threadIdx.x; k < CS; k += blockDim.x) {
+                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+                cf[k] = (double)P.in[(size_t)g * CS + k] * (double)max(1, 5 * (kx + ky + kz));
+            }
+        } else if (threadIdx.x < CS / 32) {  // fused stream decode: re-parse the cube at its marks
+            BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0};
+            r.seek(P.mark[(uint64_t)g * (CS / 32) + threadIdx.x]);
+            for (int i = 0; i < 32; i++) {
+                uint32_t code = 1u;
+                (void)r.get(code);
+                const int k = P.diag[threadIdx.x * 32 + i];
+                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+                cf[k] = (double)eg_value(code) * (double)max(1, 5 * (kx + ky + kz));
+            }
         }
         __syncthreads();
         double acc[CS / 256];
@@ -1293,6 +1364,16 @@ int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
         case 8: if (D == 8) hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, st, P); break;
         default: launch_dec_t<1>(D, groups, P, st); break;
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st) {
+    if (P.n_cubes == 0) return 0;
+    const uint32_t cpw = (D == 8) ? DecGeom<8>::CPW : DecGeom<4>::CPW;
+    const uint32_t waves = (P.n_cubes + cpw - 1) / cpw;
+    const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (D == 8) hipLaunchKernelGGL((decode_eg_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+    else hipLaunchKernelGGL((decode_eg_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P, E);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -431,6 +431,10 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     F.flag_cap = P.flag_cap;
     F.cube_list = P.cube_list;
     F.inv_coef_t = (const double*)c->d_inv_coef.p;
+    F.words = nullptr;
+    F.n_words = 0;
+    F.mark = nullptr;
+    F.diag = nullptr;
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (launch_decode_fixup(D, F, 256, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
@@ -719,15 +723,14 @@ int dct3d_eg_fetch(dct3d_ctx* c, uint8_t* out, uint64_t nbytes) {
     return DCT3D_OK;
 }
 
-int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
-                        int32_t* d_q, uint64_t* end_bit) {
-    if (!c || (n_cubes && (!d_bytes || !d_q)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+// Stream decode front: sync passes until the chunk exits converge, the scan of per-chunk code counts,
+// the mark pass (bit position of every 32nd value).  No host wait after the last pass; the caller's
+// consumer kernel (emit / fused decode) skips itself on a corrupt or short stream, and eg_decode_status
+// reports it.
+static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
+                           EgDecParams& D) {
     const uint64_t limit = nbytes * 8;
-    if (end_bit) *end_bit = start_bit;
-    if (n_cubes == 0) return DCT3D_OK;
-    if (start_bit >= limit) return DCT3D_ENODATA;
-    const uint64_t n_chunks = (limit - start_bit + 1023) / 1024;
+    const uint64_t n_chunks = (limit - start_bit + kEgChunkBits - 1) / kEgChunkBits;
     const uint64_t n_scan = (n_chunks + 4095) / 4096;
     int rc = c->d_egd_exit.grow(2 * n_chunks * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_bits.grow(n_chunks * sizeof(uint32_t));
@@ -735,7 +738,6 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
     if (!rc) rc = c->d_egd_mark.grow((n_cubes * (uint64_t)c->plan.cs / 32 + 1) * sizeof(uint64_t));
     if (rc) return rc;
-    EgDecParams D;
     D.words = (const uint32_t*)d_bytes;
     D.n_words = (nbytes + 3) / 4;
     D.start_bit = start_bit;
@@ -749,7 +751,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     D.off = (uint64_t*)c->d_eg_off.p;
     D.status = (uint64_t*)c->d_egd_status.p;
     D.mark = (uint64_t*)c->d_egd_mark.p;
-    D.q = d_q;
+    D.q = nullptr;
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts; two passes
     // are the usual total); at most n_chunks + 1 passes by induction from chunk 0
     int cur = 0;
@@ -779,7 +781,12 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
-    if (launch_eg_decode_write(c->bd, D, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_mark(D, c->stream)) return DCT3D_EKERNEL;
+    return DCT3D_OK;
+}
+
+// waits for the stream; the decode's verdict (corrupt: EINVAL, too short: ENODATA) and end bit
+static int eg_decode_status(dct3d_ctx* c, const EgDecParams& D, uint64_t* end_bit) {
     uint64_t st[4] = {0, 0, 0, 0}, total[2] = {0, 0};
     if (hipMemcpyAsync(st, c->d_egd_status.p, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipMemcpyAsync(total, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -789,6 +796,86 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if ((st[2] & 2) || total[0] < D.n_values) return DCT3D_ENODATA;
     if (end_bit) *end_bit = st[1];
     return DCT3D_OK;
+}
+
+int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
+                        int32_t* d_q, uint64_t* end_bit) {
+    if (!c || (n_cubes && (!d_bytes || !d_q)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    if (end_bit) *end_bit = start_bit;
+    if (n_cubes == 0) return DCT3D_OK;
+    if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
+    EgDecParams D;
+    int rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, D);
+    if (rc) return rc;
+    D.q = d_q;
+    if (launch_eg_emit(c->bd, D, c->stream)) return DCT3D_EKERNEL;
+    return eg_decode_status(c, D, end_bit);
+}
+
+// Fused: device stream -> device raster (the decode kernel parses its cubes at the marks; no int32
+// cube-major intermediate).  On a corrupt or short stream the decode kernel skips itself (corrupt) or
+// decodes whatever the marks hold (short: bounded windows) and the error is returned.
+int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, int w, int h,
+                        int n_stacks, uint8_t* d_raster, uint64_t* end_bit) {
+    if (!c || (n_stacks && (!d_bytes || !d_raster)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    c->last_valid = false;
+    if (end_bit) *end_bit = start_bit;
+    if (n_cubes == 0) return DCT3D_OK;
+    if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
+    EgDecParams E;
+    if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
+    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
+    const int D = c->bd;
+    const uint64_t plane = (uint64_t)w * h;
+    if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    DecodeParams P;
+    P.in = nullptr;
+    P.out = d_raster;
+    P.n_cubes = (uint32_t)n_cubes;
+    P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
+    P.nbx = (uint32_t)(w / 8);
+    P.width = (uint32_t)w;
+    P.plane = plane;
+    P.stack_stride = plane * D;
+    P.dec_G = c->plan.dec_G;
+    P.dec_E = c->plan.dec_E;
+    if (const char* e = getenv("DCT3D_DEC_MARGIN_BOOST")) P.dec_E += fabs(atof(e));  // test knob (see above)
+    P.flag_list = (unsigned long long*)c->d_flags.p;
+    P.counters = (unsigned int*)c->d_counters.p;
+    P.flag_cap = c->flag_cap;
+    P.cube_list = (uint32_t*)c->d_cubes.p;
+    hipEvent_t* ev = timing_slot(c);
+    if (ev) (void)hipEventRecord(ev[0], c->stream);
+    if (launch_decode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    DecodeFixupParams F;
+    F.in = nullptr;
+    F.out = d_raster;
+    F.cubes_per_stack = P.cubes_per_stack;
+    F.nbx = P.nbx;
+    F.width = P.width;
+    F.plane = P.plane;
+    F.stack_stride = P.stack_stride;
+    F.flag_list = P.flag_list;
+    F.counters = P.counters;
+    F.flag_cap = P.flag_cap;
+    F.cube_list = P.cube_list;
+    F.inv_coef_t = (const double*)c->d_inv_coef.p;
+    F.words = E.words;
+    F.n_words = E.n_words;
+    F.mark = E.mark;
+    F.diag = E.diag;
+    if (ev) (void)hipEventRecord(ev[2], c->stream);
+    if (launch_decode_fixup(D, F, 256, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    c->last_units = n_cubes * (uint64_t)c->plan.cs;
+    c->last_valid = true;
+    return eg_decode_status(c, E, end_bit);
 }
 
 int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int start_bit, int w, int h, int n_stacks,
@@ -801,16 +888,13 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if (end_bit) *end_bit = (uint64_t)start_bit;
     if (n_cubes == 0) return DCT3D_OK;
     const size_t px = n_cubes * c->plan.cs;
-    if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3)) || (rc = c->d_eg_q.grow(px * sizeof(int32_t))) ||
-        (rc = c->d_egd_raster.grow(px)))
+    if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3)) || (rc = c->d_egd_raster.grow(px)))
         return rc;
     if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     uint64_t eb = 0;
-    rc = dct3d_eg_decode_dev(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, (int32_t*)c->d_eg_q.p,
-                             &eb);
+    rc = dct3d_decode_eg_dev(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, w, h, n_stacks,
+                             (uint8_t*)c->d_egd_raster.p, &eb);
     if (rc) return rc;
-    if ((rc = dct3d_decode_stacks_dev(c, (const int32_t*)c->d_eg_q.p, w, h, n_stacks, (uint8_t*)c->d_egd_raster.p)))
-        return rc;
     if (hipMemcpyAsync(raster, c->d_egd_raster.p, px, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return DCT3D_EDEVICE;

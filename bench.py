@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true")
     ap.add_argument("--eg-two-step", action="store_true",
-                    help="c7: encode to int32 cube-major, then the stand-alone Exp-Golomb stage (A/B)")
+                    help="c7 / c8: the int32 cube-major intermediate plus the stand-alone Exp-Golomb stage (A/B)")
     return ap.parse_args()
 
 
@@ -176,14 +176,21 @@ def main():
         nbytes = (eg_info["bits"] + 7) // 8
         out = torch.empty_like(frames)
         eg_ev = []
-
-        def step():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            ctx.eg_decode_dev(eg_stream, nbytes, 0, n_cubes, q)  # synchronises (status read back)
-            e1.record()
-            eg_ev.append((e0, e1))
-            ctx.decode_stacks_dev(q, width, height, stacks, out)
+        if a.eg_two_step:
+            def step():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ctx.eg_decode_dev(eg_stream, nbytes, 0, n_cubes, q)  # synchronises (status read back)
+                e1.record()
+                eg_ev.append((e0, e1))
+                ctx.decode_stacks_dev(q, width, height, stacks, out)
+        else:  # fused (dct3d_decode_eg_dev): stream -> raster, no int32 intermediate
+            def step():
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ctx.decode_eg_dev(eg_stream, nbytes, 0, width, height, stacks, out)  # synchronises
+                e1.record()
+                eg_ev.append((e0, e1))
     elif direction == "encode_eg" and a.eg_two_step:
         eg_cap = n_cubes * cs  # 8 bits per value: far above what quantised content needs
         eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")
@@ -240,7 +247,11 @@ def main():
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
     fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
     achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
-    kname = "decode_kernel" if direction in ("decode", "decode_eg") else ("encode_eg_kernel" if fused else "encode_kernel")
+    fused_dec = direction == "decode_eg" and not a.eg_two_step
+    if fused_dec:  # the cube's share of the stream in, u8 out
+        bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes
+    kname = ("decode_eg_kernel" if fused_dec else "decode_kernel") if direction in ("decode", "decode_eg") else (
+        "encode_eg_kernel" if fused else "encode_kernel")
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
@@ -285,7 +296,7 @@ def main():
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,
         "eg_stage": None if direction not in ("encode_eg", "decode_eg") else {
-            "path": "decode" if direction == "decode_eg" else ("fused" if fused else "two-step"),
+            "path": ("fused" if fused_dec else "two-step") if direction == "decode_eg" else ("fused" if fused else "two-step"),
             "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
             "bits_per_value": eg_info["bits"] / (n_cubes * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},

@@ -59,7 +59,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written to it) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 3
+#define DCT3D_ABI_VERSION 4
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -212,6 +212,14 @@ int dct3d_diagonal_order(int bw, int bh, int bd, uint16_t *out);
  * leading zeros).  Synchronises the context stream. */
 int dct3d_eg_decode_dev(dct3d_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
                         int32_t *d_q, uint64_t *end_bit);
+
+/* Device stream in, device raster out, fused: decoder.c:209-295 after the inflate
+ * for n_stacks stacks -- Exp-Golomb decode, reorder, dequantisation, IDCT, clamp/truncate -- without the
+ * int32 cube-major intermediate: the decode kernel parses each of its cubes from the stream directly.
+ * Stream arguments, *end_bit and errors as dct3d_eg_decode_dev; the raster as dct3d_decode_stacks_dev.
+ * Synchronises the context stream. */
+int dct3d_decode_eg_dev(dct3d_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint64_t start_bit, int width,
+                        int height, int n_stacks, uint8_t *d_raster, uint64_t *end_bit);
 
 /* Host stream in, raster out: decoder.c:209-295 after the inflate -- Exp-Golomb decode, reorder,
  * dequantisation, IDCT, clamp/truncate and writeCubes for n_stacks stacks, on the device; only the

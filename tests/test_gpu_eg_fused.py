@@ -124,3 +124,85 @@ def test_host_encode_eg_is_fused_and_identical(pkg, gpu_ctx8, gpu_ctx4, depth):
     ref, rbits, _ = _gpu_stream(ctx, q, 0x80, 1)
     got, tb = ctx.encode_eg(fr, 0x80, 1)
     assert tb == rbits and got == ref
+
+
+# ------------------------------------------------------------------------------------------------
+# fused stream -> raster decode (dct3d_decode_eg_dev)
+# ------------------------------------------------------------------------------------------------
+def _stream_dev(data: bytes):
+    import torch
+    n = (len(data) + 3) // 4 + 1
+    buf = np.zeros(n * 4, np.uint8)
+    buf[: len(data)] = np.frombuffer(data, np.uint8)
+    return torch.from_numpy(buf).cuda()
+
+
+def _decode_fused(ctx, data: bytes, w, h, stacks, start_bit=0):
+    import torch
+    d = _stream_dev(data)
+    out = torch.empty((stacks * ctx.bd, h, w), dtype=torch.uint8, device="cuda")
+    eb = ctx.decode_eg_dev(d, len(data), start_bit, w, h, stacks, out)
+    return out.cpu().numpy(), eb
+
+
+def _decode_two_step(ctx, data: bytes, w, h, stacks, start_bit=0):
+    import torch
+    d = _stream_dev(data)
+    n = ctx.n_cubes(w, h, stacks)
+    q = torch.empty(n * ctx.cube_size, dtype=torch.int32, device="cuda")
+    eb = ctx.eg_decode_dev(d, len(data), start_bit, n, q)
+    out = torch.empty((stacks * ctx.bd, h, w), dtype=torch.uint8, device="cuda")
+    ctx.decode_stacks_dev(q, w, h, stacks, out)
+    return out.cpu().numpy(), eb
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["ramp", "uniform"])
+def test_fused_decode_1080p_matches_two_step(pkg, gpu_ctx8, gpu_ctx4, depth, kind):
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = pkg.synthetic.frames(1920, 1080, 2 * depth, kind=kind, frame0=5)
+    data, tb = ctx.encode_eg(fr)
+    ref, reb = _decode_two_step(ctx, data, 1920, 1080, 2)
+    got, eb = _decode_fused(ctx, data, 1920, 1080, 2)
+    assert eb == reb == tb
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["ramp", "uniform", "checker", "full"])
+def test_fused_decode_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, kind):
+    """stream of the oracle's cubes -> fused decode == the oracle's Java-semantics decode of the cubes"""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    fr = _content(pkg, kind, 64, 48, 2 * depth)
+    q = plan.encode_q(fr)
+    data, nbits = _expected(oracle, pkg, q, depth, 0xC0, 3)    # starts at bit 3 of a carried byte
+    got, eb = _decode_fused(ctx, data, 64, 48, 2, start_bit=3)
+    assert eb == nbits
+    assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
+
+
+def test_fused_decode_whole_cube_replay_from_stream(pkg, gpu_ctx8, monkeypatch):
+    """a widened certification margin sends cubes to the replay, which re-parses them from the stream"""
+    fr = pkg.synthetic.frames(256, 128, 16, kind="uniform", frame0=9)
+    data, _ = gpu_ctx8.encode_eg(fr)
+    ref, _ = _decode_two_step(gpu_ctx8, data, 256, 128, 2)
+    monkeypatch.setenv("DCT3D_DEC_MARGIN_BOOST", "0.45")
+    got, _ = _decode_fused(gpu_ctx8, data, 256, 128, 2)
+    assert gpu_ctx8.stats()["n_overflow_cubes"] > 0       # the replay path ran
+    assert np.array_equal(got, ref)
+
+
+def test_fused_decode_truncated_and_corrupt(pkg, gpu_ctx8):
+    fr = pkg.synthetic.frames(128, 64, 16, kind="uniform", frame0=2)
+    data, _ = gpu_ctx8.encode_eg(fr)
+    with pytest.raises(pkg.Dct3dError) as e:
+        _decode_fused(gpu_ctx8, data[: len(data) // 2], 128, 64, 2)
+    assert e.value.code == pkg.DCT3D_ENODATA
+    got, _ = _decode_fused(gpu_ctx8, data[: len(data) // 2 + len(data) // 8], 128, 64, 1)   # one stack is there
+    ref, _ = _decode_two_step(gpu_ctx8, data, 128, 64, 1)
+    assert np.array_equal(got, ref)
+    bad = bytearray(data)
+    bad[len(bad) // 3: len(bad) // 3 + 6] = bytes(6)                    # 48 zero bits: no valid code
+    with pytest.raises(pkg.Dct3dError) as e:
+        _decode_fused(gpu_ctx8, bytes(bad), 128, 64, 2)
+    assert e.value.code in (pkg.DCT3D_EINVAL, pkg.DCT3D_ENODATA)
