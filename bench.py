@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import importlib
 import json
+import math
 import os
 import sys
 import time
@@ -234,6 +235,14 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
     ctx.set_profiling(False)
+    round_trip = None
+    if direction in ("decode", "decode_eg"):  # the codec's round trip on this GPU's frames
+        d = out.to(torch.int16) - frames.to(torch.int16)
+        mse = float((d.to(torch.float64) ** 2).mean())
+        round_trip = {"vs": "encoder input frames (lossy: quantisation); bit-exactness against the Java-semantics "
+                            "decode is pinned by tests/test_gpu_parity.py",
+                      "max_abs_err": int(d.abs().max()), "mean_abs_err": float(d.abs().to(torch.float64).mean()),
+                      "psnr_db": (10.0 * math.log10(255.0 ** 2 / mse)) if mse > 0 else None}
     ceiling = None if a.no_ceiling or q is None else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
     sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
     elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
@@ -300,6 +309,7 @@ def main():
             "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
             "bits_per_value": eg_info["bits"] / (n_cubes * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
+        "round_trip": round_trip,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
