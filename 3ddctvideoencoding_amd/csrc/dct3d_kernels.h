@@ -47,6 +47,7 @@ struct DecodeParams {
     const int32_t* in;
     uint8_t* out;
     uint32_t n_cubes, cubes_per_stack, nbx, width;
+    uint32_t cube_base;        // decode_eg_kernel: first cube of this launch (a chunk of whole stacks)
     uint64_t plane, stack_stride;
     double dec_G, dec_E;
     unsigned long long* flag_list;

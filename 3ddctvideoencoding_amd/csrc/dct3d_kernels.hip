@@ -1011,7 +1011,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * CPW;
+    const uint32_t cube0 = P.cube_base + (blockIdx.x * kWavesPerBlock + wave) * CPW;
     if (cube0 >= P.n_cubes) return;
     const uint64_t n_marks = E.n_values / 32;
     const uint64_t m0 = (uint64_t)cube0 * CS / 32;
@@ -1370,7 +1370,7 @@ int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
 int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     const uint32_t cpw = (D == 8) ? DecGeom<8>::CPW : DecGeom<4>::CPW;
-    const uint32_t waves = (P.n_cubes + cpw - 1) / cpw;
+    const uint32_t waves = (P.n_cubes - P.cube_base + cpw - 1) / cpw;  // cube_base: a multiple of cpw
     const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
     if (D == 8) hipLaunchKernelGGL((decode_eg_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P, E);
     else hipLaunchKernelGGL((decode_eg_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P, E);

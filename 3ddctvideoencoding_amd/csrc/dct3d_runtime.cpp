@@ -13,6 +13,9 @@
 #include <vector>
 #include <cstring>
 #include <mutex>
+#include <condition_variable>
+#include <deque>
+#include <thread>
 #include <new>
 
 #include "../../include/dct3d.h"
@@ -72,6 +75,10 @@ struct dct3d_ctx {
     DevBuf d_egf_slot, d_egf_lbits;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
+    // host-pointer pipeline: copy streams, slot events, double-buffered slots
+    hipStream_t s_up = nullptr, s_down = nullptr;
+    hipEvent_t pe_in[2] = {}, pe_done[2] = {};
+    DevBuf p_in[2], p_out[2];
     uint64_t eg_last_bytes = 0;
 };
 
@@ -203,6 +210,12 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     for (auto& q : c->ev)
         for (auto& e : q)
             if (e) (void)hipEventDestroy(e);
+    if (c->s_up) (void)hipStreamDestroy(c->s_up);
+    if (c->s_down) (void)hipStreamDestroy(c->s_down);
+    for (int i = 0; i < 2; i++) {
+        if (c->pe_in[i]) (void)hipEventDestroy(c->pe_in[i]);
+        if (c->pe_done[i]) (void)hipEventDestroy(c->pe_done[i]);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -400,6 +413,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     P.in = d_q;
     P.out = d_raster;
     P.n_cubes = (uint32_t)n_cubes;
+    P.cube_base = 0;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
     P.width = (uint32_t)w;
@@ -443,6 +457,113 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     return DCT3D_OK;
 }
 
+// ---- host-pointer pipeline ------------------------------------------------------
+// The host entry points move whole stacks in chunks: chunk i's upload (copy stream s_up, issued here),
+// its kernels (the context stream, after the upload's event) and its download (copy stream s_down,
+// issued by a helper thread: a D2H copy into pageable memory blocks the thread that issues it) overlap
+// with chunk i+1's upload and chunk i-1's download.  PCIe is full duplex (~57 GB/s each way measured,
+// pinned or pageable), so a call approaches max(in, out) / link rate instead of (in + out) / rate.
+// Two device slots per direction; chunk i reuses slot i & 1 after chunk i-2's kernels (event) and
+// download (the helper has returned from it) are done.  Synchronous on return, like the reference.
+}  // extern "C" (the pipeline helpers are C++ templates)
+static int ensure_pipe(dct3d_ctx* c) {
+    if (c->s_up) return DCT3D_OK;
+    if (hipStreamCreateWithFlags(&c->s_up, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->s_down, hipStreamNonBlocking) != hipSuccess)
+        return DCT3D_EDEVICE;
+    for (int i = 0; i < 2; i++)
+        if (hipEventCreateWithFlags(&c->pe_in[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->pe_done[i], hipEventDisableTiming) != hipSuccess)
+            return DCT3D_EDEVICE;
+    return DCT3D_OK;
+}
+
+static int chunk_stacks_for(size_t bytes_per_stack, int n_stacks) {
+    // ~64 MB per chunk on the heavier side, at least 1 stack, at most n_stacks / 2 (some overlap)
+    size_t k = (64u << 20) / (bytes_per_stack ? bytes_per_stack : 1);
+    if (k < 1) k = 1;
+    const int half = n_stacks > 1 ? (n_stacks + 1) / 2 : 1;
+    return (int)(k < (size_t)half ? k : (size_t)half);
+}
+
+// compute(d_in, d_out, first_stack, stacks) enqueues one chunk's kernels on c->stream
+template <class Compute>
+static int run_pipeline(dct3d_ctx* c, int n_stacks, size_t in_per_stack, size_t out_per_stack, const void* host_in,
+                        void* host_out, Compute&& compute) {
+    int rc = ensure_pipe(c);
+    if (rc) return rc;
+    const int cst = chunk_stacks_for(in_per_stack > out_per_stack ? in_per_stack : out_per_stack, n_stacks);
+    const int n_chunks = (n_stacks + cst - 1) / cst;
+    for (int s = 0; s < 2; s++)
+        if ((in_per_stack && (rc = c->p_in[s].grow(cst * in_per_stack))) || (rc = c->p_out[s].grow(cst * out_per_stack)))
+            return rc;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<int> todo;
+    int downloaded = 0;  // chunks whose download has completed
+    bool closing = false, failed = false;
+    std::thread helper([&] {
+        if (hipSetDevice(c->device) != hipSuccess) {
+            std::lock_guard<std::mutex> lk(mu);
+            failed = true;
+        }
+        for (;;) {
+            int i;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !todo.empty() || closing; });
+                if (todo.empty()) return;
+                i = todo.front();
+                todo.pop_front();
+            }
+            const int s = i & 1, st0 = i * cst, ns = (st0 + cst <= n_stacks) ? cst : n_stacks - st0;
+            bool ok = !failed && hipStreamWaitEvent(c->s_down, c->pe_done[s], 0) == hipSuccess &&
+                      hipMemcpyAsync((char*)host_out + (size_t)st0 * out_per_stack, c->p_out[s].p, ns * out_per_stack,
+                                     hipMemcpyDeviceToHost, c->s_down) == hipSuccess &&
+                      hipStreamSynchronize(c->s_down) == hipSuccess;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (!ok) failed = true;
+                downloaded++;
+            }
+            cv.notify_all();
+        }
+    });
+    for (int i = 0; i < n_chunks && rc == DCT3D_OK; i++) {
+        const int s = i & 1, st0 = i * cst, ns = (st0 + cst <= n_stacks) ? cst : n_stacks - st0;
+        if (host_in) {  // (no upload when the input is already on the device)
+            if (i >= 2 && hipStreamWaitEvent(c->s_up, c->pe_done[s], 0) != hipSuccess) rc = DCT3D_EDEVICE;
+            if (!rc && (hipMemcpyAsync(c->p_in[s].p, (const char*)host_in + (size_t)st0 * in_per_stack,
+                                       ns * in_per_stack, hipMemcpyHostToDevice, c->s_up) != hipSuccess ||
+                        hipEventRecord(c->pe_in[s], c->s_up) != hipSuccess ||
+                        hipStreamWaitEvent(c->stream, c->pe_in[s], 0) != hipSuccess))
+                rc = DCT3D_EDEVICE;
+        }
+        {  // slot s's previous download (chunk i - 2) must be finished before its kernels overwrite it
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return downloaded >= i - 1 || failed; });
+            if (failed) rc = DCT3D_EDEVICE;
+        }
+        if (!rc) rc = compute(c->p_in[s].p, c->p_out[s].p, st0, ns);
+        if (!rc && hipEventRecord(c->pe_done[s], c->stream) != hipSuccess) rc = DCT3D_EDEVICE;
+        if (!rc) {
+            std::lock_guard<std::mutex> lk(mu);
+            todo.push_back(i);
+        }
+        cv.notify_all();
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        closing = true;
+    }
+    cv.notify_all();
+    helper.join();
+    if (failed && !rc) rc = DCT3D_EDEVICE;
+    if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = DCT3D_EDEVICE;
+    return rc;
+}
+
+extern "C" {
 // ---- host-pointer entry points (synchronous; the reference's blocking transfers) ----------------
 int dct3d_encode_stacks(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n_stacks, int32_t* q, double* dct) {
     if (!c || (!raster && n_stacks) || (!q && n_stacks)) return DCT3D_EINVAL;
@@ -452,6 +573,13 @@ int dct3d_encode_stacks(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     if (n_cubes == 0) return DCT3D_OK;
     const size_t in_bytes = n_cubes * c->plan.cs, out_bytes = in_bytes * sizeof(int32_t);
+    if (!dct) {  // pipelined
+        const size_t px = in_bytes / n_stacks;
+        return run_pipeline(c, n_stacks, px, px * sizeof(int32_t), raster, q,
+                            [&](const void* din, void* dout, int, int ns) {
+                                return dct3d_encode_stacks_dev(c, (const uint8_t*)din, w, h, ns, (int32_t*)dout, nullptr);
+                            });
+    }
     if ((rc = c->h_in.grow(in_bytes)) || (rc = c->h_out.grow(out_bytes))) return rc;
     if (hipMemcpyAsync(c->h_in.p, raster, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     if (dct && (rc = c->h_aux.grow(in_bytes * sizeof(double)))) return rc;
@@ -471,13 +599,10 @@ int dct3d_decode_stacks(dct3d_ctx* c, const int32_t* q, int w, int h, int n_stac
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     if (n_cubes == 0) return DCT3D_OK;
-    const size_t px = n_cubes * c->plan.cs, in_bytes = px * sizeof(int32_t);
-    if ((rc = c->h_in.grow(in_bytes)) || (rc = c->h_out.grow(px))) return rc;
-    if (hipMemcpyAsync(c->h_in.p, q, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    rc = dct3d_decode_stacks_dev(c, (const int32_t*)c->h_in.p, w, h, n_stacks, (uint8_t*)c->h_out.p);
-    if (rc) return rc;
-    if (hipMemcpyAsync(raster, c->h_out.p, px, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    return hipStreamSynchronize(c->stream) == hipSuccess ? DCT3D_OK : DCT3D_EDEVICE;
+    const size_t px = n_cubes * c->plan.cs / n_stacks;
+    return run_pipeline(c, n_stacks, px * sizeof(int32_t), px, q, raster, [&](const void* din, void* dout, int, int ns) {
+        return dct3d_decode_stacks_dev(c, (const int32_t*)din, w, h, ns, (uint8_t*)dout);
+    });
 }
 
 // ---- drop-in (A): float cube-major <-> float cube-major --------------------------------------
@@ -813,31 +938,23 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     return eg_decode_status(c, D, end_bit);
 }
 
-// Fused: device stream -> device raster (the decode kernel parses its cubes at the marks; no int32
-// cube-major intermediate).  On a corrupt or short stream the decode kernel skips itself (corrupt) or
-// decodes whatever the marks hold (short: bounded windows) and the error is returned.
-int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, int w, int h,
-                        int n_stacks, uint8_t* d_raster, uint64_t* end_bit) {
-    if (!c || (n_stacks && (!d_bytes || !d_raster)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
-    uint64_t n_cubes;
-    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
-    if (rc) return rc;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    c->last_valid = false;
-    if (end_bit) *end_bit = start_bit;
-    if (n_cubes == 0) return DCT3D_OK;
-    if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
-    EgDecParams E;
-    if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
-    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
+// Fused stream -> raster decode of stacks [st0, st0 + ns) after eg_decode_front: the decode kernel parses
+// its cubes at the marks (no int32 cube-major intermediate), the fixup replays flagged cubes by
+// re-parsing them.  out_stack0 = where stack st0 goes (the raster pointer is rebased so that the
+// kernels' global cube indices land in it).
+}  // extern "C"
+static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int st0, int ns, uint8_t* out_stack0) {
     const int D = c->bd;
     const uint64_t plane = (uint64_t)w * h;
+    const uint64_t cps = (uint64_t)(w / 8) * (h / 8);
+    uint8_t* out = out_stack0 - (size_t)st0 * plane * D;  // rebased: stack st0 at out_stack0
     if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     DecodeParams P;
     P.in = nullptr;
-    P.out = d_raster;
-    P.n_cubes = (uint32_t)n_cubes;
-    P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
+    P.out = out;
+    P.cube_base = (uint32_t)(st0 * cps);
+    P.n_cubes = (uint32_t)((st0 + ns) * cps);
+    P.cubes_per_stack = (uint32_t)cps;
     P.nbx = (uint32_t)(w / 8);
     P.width = (uint32_t)w;
     P.plane = plane;
@@ -855,7 +972,7 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     DecodeFixupParams F;
     F.in = nullptr;
-    F.out = d_raster;
+    F.out = out;
     F.cubes_per_stack = P.cubes_per_stack;
     F.nbx = P.nbx;
     F.width = P.width;
@@ -873,6 +990,27 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (launch_decode_fixup(D, F, 256, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
+    return DCT3D_OK;
+}
+extern "C" {
+
+// Fused: device stream -> device raster.  On a corrupt stream the decode kernel skips itself; on a short
+// one it decodes whatever the marks hold (bounded windows); the error is returned either way.
+int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, int w, int h,
+                        int n_stacks, uint8_t* d_raster, uint64_t* end_bit) {
+    if (!c || (n_stacks && (!d_bytes || !d_raster)) || ((uintptr_t)d_bytes & 3)) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    c->last_valid = false;
+    if (end_bit) *end_bit = start_bit;
+    if (n_cubes == 0) return DCT3D_OK;
+    if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
+    EgDecParams E;
+    if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
+    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
+    if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = true;
     return eg_decode_status(c, E, end_bit);
@@ -887,19 +1025,21 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     if (end_bit) *end_bit = (uint64_t)start_bit;
     if (n_cubes == 0) return DCT3D_OK;
-    const size_t px = n_cubes * c->plan.cs;
-    if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3)) || (rc = c->d_egd_raster.grow(px)))
-        return rc;
+    if ((uint64_t)start_bit >= nbytes * 8) return DCT3D_ENODATA;
+    if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3))) return rc;
     if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    uint64_t eb = 0;
-    rc = dct3d_decode_eg_dev(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, w, h, n_stacks,
-                             (uint8_t*)c->d_egd_raster.p, &eb);
+    EgDecParams E;
+    if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E))) return rc;
+    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
+    // the raster leaves in chunks of stacks while the next chunk decodes (the stream is small: no upload)
+    const size_t px = n_cubes * c->plan.cs / n_stacks;
+    rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
+        return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
+    });
     if (rc) return rc;
-    if (hipMemcpyAsync(raster, c->d_egd_raster.p, px, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return DCT3D_EDEVICE;
-    if (end_bit) *end_bit = eb;
-    return DCT3D_OK;
+    c->last_units = n_cubes * (uint64_t)c->plan.cs;
+    c->last_valid = true;
+    return eg_decode_status(c, E, end_bit);
 }
 
 }  // extern "C"
