@@ -39,6 +39,10 @@ constexpr int kSlot = 144;                 // transpose slot: 8 rows x 16 B + 16
 constexpr int kWaveLds = kSlot * 64;       // 9216 B per wave
 constexpr int kFace = 272;                 // staging face: 256 B + 16 B pad
 static_assert(4 * 8 * kFace <= kWaveLds, "staging round must fit the wave region");
+// per-wave LDS of the encode kernels: 8x8x4 moves its transpose and staging in two half rounds
+// (4.5 KiB), so that LDS does not cap it at 16 waves per CU (it needs 96 VGPRs: 5 waves per SIMD)
+template <int D> constexpr int enc_wave_lds() { return D == 8 ? kWaveLds : kWaveLds / 2; }
+static_assert(4 * 4 * kFace <= kWaveLds / 2, "8x8x4 staging round must fit the half region");
 
 // Wave-level ordering of LDS traffic between lanes of ONE wave: a compiler fence (LDS instructions
 // of a wave are executed in order, so no s_waitcnt is needed for visibility within the wave).
@@ -199,19 +203,23 @@ __device__ __forceinline__ void forward_cube(float (&a)[D][8], int m, int c, int
             wave_lds_sync();
         }
     } else {
+        // two rounds (x halves h): every lane writes its rows' half h; the lanes owning kx half h read
 #pragma unroll
-        for (int kz = 0; kz < 4; kz++)
+        for (int h = 0; h < 2; h++) {
 #pragma unroll
-            for (int h = 0; h < 2; h++)
-                *(float4*)(wl + ((c * 4 + kz) * 2 + h) * kSlot + j * 16) =
+            for (int kz = 0; kz < 4; kz++)
+                *(float4*)(wl + (c * 4 + kz) * kSlot + j * 16) =
                     make_float4(a[kz][4 * h], a[kz][4 * h + 1], a[kz][4 * h + 2], a[kz][4 * h + 3]);
-        wave_lds_sync();
+            wave_lds_sync();
+            if ((j & 1) == h) {
 #pragma unroll
-        for (int y = 0; y < 8; y++) {
-            float4 t = *(const float4*)(wl + (c * 8 + j) * kSlot + y * 16);
-            b[y][0] = t.x; b[y][1] = t.y; b[y][2] = t.z; b[y][3] = t.w;
+                for (int y = 0; y < 8; y++) {
+                    float4 t = *(const float4*)(wl + (c * 4 + (j >> 1)) * kSlot + y * 16);
+                    b[y][0] = t.x; b[y][1] = t.y; b[y][2] = t.z; b[y][3] = t.w;
+                }
+            }
+            wave_lds_sync();
         }
-        wave_lds_sync();
     }
     // pass Y
     {
@@ -318,8 +326,9 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
     if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
 
     // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
-    constexpr int ROUNDS = (D == 8) ? 2 : 1;
+    constexpr int ROUNDS = 2;
     constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
+    constexpr int CHUNK_ITERS = CUBES_PER_ROUND * (CS / 4) / 64;  // 16-byte chunks per lane per round
 #pragma unroll
     for (int rd = 0; rd < ROUNDS; rd++) {
         if ((c / CUBES_PER_ROUND) == rd) {
@@ -342,8 +351,8 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
         const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
         char* outb = (char*)(P.out + (size_t)rcube0 * CS);
 #pragma unroll
-        for (int t = 0; t < 8; t++) {
-            const int q = t * 64 + lane;                 // 16-byte chunk within the 8 KiB round
+        for (int t = 0; t < CHUNK_ITERS; t++) {
+            const int q = t * 64 + lane;                 // 16-byte chunk within the round
             const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
             const int face = (q >> 4) % D;
             const int w = q & 15;
@@ -397,12 +406,12 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
 // and were 25-40 % slower: profiles/r01/encode_variant_sweep.txt).
 template <int D, bool NT, bool NTL = false>
 __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
     uint2 raw[D];
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
-    if (cube0 < P.n_cubes) encode_body<D, NT>(P, raw, lds + wave * kWaveLds, lane, cube0);  // wave-uniform
+    if (cube0 < P.n_cubes) encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), lane, cube0);  // wave-uniform
 }
 
 // =============================================================================================
@@ -521,8 +530,8 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     constexpr int NI = 7 + NB;
     constexpr int VPL = CS / 8;            // stream values per lane
     constexpr int CUBE_B = 2 * CS + 16;    // int16 cube-major staging per cube (+16 B: bank spread)
-    static_assert(8 * CUBE_B <= kWaveLds, "int16 staging must fit the wave region");
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kWaveLds];
+    static_assert(8 * CUBE_B <= enc_wave_lds<D>(), "int16 staging must fit the wave region");
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
     __shared__ int rs_sum[kWavesPerBlock][kMaxGroupsDev];
     __shared__ double rs_prod[kWavesPerBlock][kMaxGroupsDev];
     __shared__ __attribute__((aligned(16))) uint16_t s_pos[CS];  // stream position -> byte offset in a cube
@@ -534,7 +543,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     for (int i = threadIdx.x; i < CS; i += kBlock) s_pos[i] = (uint16_t)(2 * E.diag[i]);
     __syncthreads();
     if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
-    char* wl = lds + wave * kWaveLds;
+    char* wl = lds + wave * enc_wave_lds<D>();
     const int c = lane >> 3, j = lane & 7;
     const int kz = (D == 8) ? j : (j >> 1);
     const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
