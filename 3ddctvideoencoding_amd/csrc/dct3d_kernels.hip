@@ -733,11 +733,13 @@ __device__ __forceinline__ uint32_t cvt_u32_sat(double v) {
 }
 
 // staged input of one tile (CPW cubes, 8 KiB): 8 coalesced 1 KiB loads per wave
+// (4-byte values: int32 quantised cubes, or the float cubes of the drop-in kernels)
 template <int D>
-__device__ __forceinline__ void dec_load_tile(const DecodeParams& P, uint32_t cube0, int lane, int4 (&v)[8]) {
+__device__ __forceinline__ void dec_load_tile_p(const char* in, uint32_t n_cubes, uint32_t cube0, int lane,
+                                                int4 (&v)[8]) {
     using G = DecGeom<D>;
-    const char* inb = (const char*)(P.in + (size_t)cube0 * G::CS);
-    if (cube0 + G::CPW <= P.n_cubes) {  // wave-uniform: every cube of the tile exists
+    const char* inb = in + (size_t)cube0 * G::CS * 4;
+    if (cube0 + G::CPW <= n_cubes) {  // wave-uniform: every cube of the tile exists
 #pragma unroll
         for (int t = 0; t < 8; t++) v[t] = *(const int4*)(inb + (size_t)(t * 64 + lane) * 16);
     } else {
@@ -745,9 +747,13 @@ __device__ __forceinline__ void dec_load_tile(const DecodeParams& P, uint32_t cu
         for (int t = 0; t < 8; t++) {
             const int q = t * 64 + lane;
             v[t] = make_int4(0, 0, 0, 0);
-            if (cube0 + q / (G::CS / 4) < P.n_cubes) v[t] = *(const int4*)(inb + (size_t)q * 16);
+            if (cube0 + q / (G::CS / 4) < n_cubes) v[t] = *(const int4*)(inb + (size_t)q * 16);
         }
     }
+}
+template <int D>
+__device__ __forceinline__ void dec_load_tile(const DecodeParams& P, uint32_t cube0, int lane, int4 (&v)[8]) {
+    dec_load_tile_p<D>((const char*)P.in, P.n_cubes, cube0, lane, v);
 }
 template <int D>
 __device__ __forceinline__ void dec_stage_tile(char* wl, int lane, const int4 (&v)[8]) {
@@ -756,6 +762,57 @@ __device__ __forceinline__ void dec_stage_tile(char* wl, int lane, const int4 (&
     for (int t = 0; t < 8; t++) {
         const int q = t * 64 + lane;
         *(int4*)(wl + (q / (G::CS / 4)) * G::SA_C + ((q >> 4) % D) * G::SA_F + (q & 15) * 16) = v[t];
+    }
+}
+
+// ---- B -> C through LDS in two rounds (D=8: z halves, D=4: x halves); every lane reads in
+//      every round into fixed registers (no lane-divergent definitions to merge) ----
+//   in:  layout B, lane (c, kz=k, h): row r (y = 4h + r): x 0..3 in b[r][.], x 4..7 in b[4 + r][.]
+//   out: layout C, D=8: lane (c, y=k, h) cz[z][e] (x = 4h + e); D=4: lane (c, y=4h+k) cz[z][x]
+template <int D>
+__device__ __forceinline__ void dec_b_to_c(const double (&b)[8][4], double (&cz)[D][(D == 8) ? 4 : 8], char* wl,
+                                           int c, int k, int h) {
+    using G = DecGeom<D>;
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {
+        wave_lds_sync();
+        if constexpr (D == 8) {
+            if ((k >> 2) == rd) {  // writers: this round's z half; rows of 8 x (64 B)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    char* dst = wl + c * G::TC + (k & 3) * G::TZ + (4 * h + r) * 64;
+                    *(double2*)(dst) = make_double2(b[r][0], b[r][1]);
+                    *(double2*)(dst + 16) = make_double2(b[r][2], b[r][3]);
+                    *(double2*)(dst + 32) = make_double2(b[4 + r][0], b[4 + r][1]);
+                    *(double2*)(dst + 48) = make_double2(b[4 + r][2], b[4 + r][3]);
+                }
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int zr = 0; zr < 4; zr++) {
+                const char* src = wl + c * G::TC + zr * G::TZ + k * 64 + h * 32;
+                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
+                cz[4 * rd + zr][0] = t0.x; cz[4 * rd + zr][1] = t0.y;
+                cz[4 * rd + zr][2] = t1.x; cz[4 * rd + zr][3] = t1.y;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const double* sv = (rd == 0) ? b[r] : b[4 + r];
+                char* dst = wl + c * G::TC + k * G::TZ + G::tslot(k, 4 * h + r) * 32;
+                *(double2*)(dst) = make_double2(sv[0], sv[1]);
+                *(double2*)(dst + 16) = make_double2(sv[2], sv[3]);
+            }
+            wave_lds_sync();
+            const int y = 4 * h + k;
+#pragma unroll
+            for (int z = 0; z < 4; z++) {
+                const char* src = wl + c * G::TC + z * G::TZ + G::tslot(z, y) * 32;
+                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
+                cz[z][4 * rd + 0] = t0.x; cz[z][4 * rd + 1] = t0.y;
+                cz[z][4 * rd + 2] = t1.x; cz[z][4 * rd + 3] = t1.y;
+            }
+        }
     }
 }
 
@@ -873,50 +930,8 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             }
     }
 
-    // ---- B -> C through LDS in two rounds (D=8: z halves, D=4: x halves); every lane reads in
-    //      every round into fixed registers (no lane-divergent definitions to merge) ----
     double cz[D][NXC];
-#pragma unroll
-    for (int rd = 0; rd < 2; rd++) {
-        wave_lds_sync();
-        if constexpr (D == 8) {
-            if ((k >> 2) == rd) {  // writers: this round's z half; rows of 8 x (64 B)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    char* dst = wl + c * G::TC + (k & 3) * G::TZ + (4 * h + r) * 64;
-                    *(double2*)(dst) = make_double2(b[r][0], b[r][1]);
-                    *(double2*)(dst + 16) = make_double2(b[r][2], b[r][3]);
-                    *(double2*)(dst + 32) = make_double2(b[4 + r][0], b[4 + r][1]);
-                    *(double2*)(dst + 48) = make_double2(b[4 + r][2], b[4 + r][3]);
-                }
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int zr = 0; zr < 4; zr++) {
-                const char* src = wl + c * G::TC + zr * G::TZ + k * 64 + h * 32;
-                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
-                cz[4 * rd + zr][0] = t0.x; cz[4 * rd + zr][1] = t0.y;
-                cz[4 * rd + zr][2] = t1.x; cz[4 * rd + zr][3] = t1.y;
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const double* sv = (rd == 0) ? b[r] : b[4 + r];
-                char* dst = wl + c * G::TC + k * G::TZ + G::tslot(k, 4 * h + r) * 32;
-                *(double2*)(dst) = make_double2(sv[0], sv[1]);
-                *(double2*)(dst + 16) = make_double2(sv[2], sv[3]);
-            }
-            wave_lds_sync();
-            const int y = 4 * h + k;
-#pragma unroll
-            for (int z = 0; z < 4; z++) {
-                const char* src = wl + c * G::TC + z * G::TZ + G::tslot(z, y) * 32;
-                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
-                cz[z][4 * rd + 0] = t0.x; cz[z][4 * rd + 1] = t0.y;
-                cz[z][4 * rd + 2] = t1.x; cz[z][4 * rd + 3] = t1.y;
-            }
-        }
-    }
+    dec_b_to_c<D>(b, cz, wl, c, k, h);
 
     // ---- inverse pass Z ----
     constexpr int G3 = PG == 0 ? NXC : PG;
@@ -1000,6 +1015,134 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     dec_stage_tile<D>(wl, lane, v);
     wave_lds_sync();
     decode_tile<D, PG>(P, wl, lane, cube0, [] {});
+}
+
+// =============================================================================================
+// Drop-in (A): float cube-major -> float cube-major, fp64 internal (3dDCT.cl:43-143 / 164-265)
+// =============================================================================================
+// The decode kernel's geometry (2*D lanes per cube, 32 doubles per lane, staged 1 KiB loads, the
+// lane-pair swap and the two LDS rounds), with the forward (DCT-II) or inverse (DCT-III, clamped to
+// [0,255] as 3dDCT.cl:257-261) butterflies along Y, X, Z.  Layout C stores f32 cube-major directly:
+// for D = 8 a store instruction covers one 256-byte z face of each of the wave's 4 cubes.
+template <bool INV>
+__device__ __forceinline__ void f64_line8(double (&x)[8]) {
+    if constexpr (INV) idct8(x);
+    else fdct8<false, false>(x, 0.0);
+}
+template <int D, bool INV>
+__global__ __launch_bounds__(kBlock, 4) void cube_f32_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                             uint32_t n_cubes) {
+    using G = DecGeom<D>;
+    constexpr int CPW = G::CPW;
+    constexpr int NXC = (D == 8) ? 4 : 8;
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    char* wl = lds + wave * kDecWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * CPW;
+    if (cube0 >= n_cubes) return;  // wave-uniform
+    {
+        int4 v[8];
+        dec_load_tile_p<D>((const char*)in, n_cubes, cube0, lane, v);
+        dec_stage_tile<D>(wl, lane, v);
+    }
+    wave_lds_sync();
+    const int h = (lane >> 4) & 1, k = lane & (D - 1);
+    const int c = (lane >> 5) * (CPW / 2) + ((lane & 15) / D);
+    const uint32_t g = cube0 + c;
+
+    // layout A: lane (c, z = k, h) holds face k, rows y, x = 4h + e
+    double b[8][4];
+    {
+        const char* src = wl + c * G::SA_C + k * G::SA_F + h * 16;
+        float4 raw[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) raw[y] = *(const float4*)(src + y * 32);
+#pragma unroll
+        for (int y = 0; y < 8; y++) {
+            b[y][0] = raw[y].x; b[y][1] = raw[y].y; b[y][2] = raw[y].z; b[y][3] = raw[y].w;
+        }
+    }
+    // pass Y
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        double col[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = b[y][e];
+        pin(col);
+        f64_line8<INV>(col);
+        pin(col);
+#pragma unroll
+        for (int y = 0; y < 8; y++) b[y][e] = col[y];
+    }
+    // A -> B: lane-pair swap of the off-diagonal 4x4 blocks
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) swap16(b[r][e], b[4 + r][e]);
+    // pass X
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        double row[8];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            row[e] = b[r][e];
+            row[4 + e] = b[4 + r][e];
+        }
+        pin(row);
+        f64_line8<INV>(row);
+        pin(row);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            b[r][e] = row[e];
+            b[4 + r][e] = row[4 + e];
+        }
+    }
+    double cz[D][NXC];
+    dec_b_to_c<D>(b, cz, wl, c, k, h);
+    // pass Z
+#pragma unroll
+    for (int e = 0; e < NXC; e++) {
+        double col[D];
+#pragma unroll
+        for (int z = 0; z < D; z++) col[z] = cz[z][e];
+        pin(col);
+        if constexpr (INV) idctN<D>(col);
+        else fdctN<D, false, false>(col, 0.0);
+        pin(col);
+#pragma unroll
+        for (int z = 0; z < D; z++) cz[z][e] = col[z];
+    }
+    if (g < n_cubes) {
+        const int y = (D == 8) ? k : (4 * h + k);
+        const int x0 = (D == 8) ? 4 * h : 0;
+        float* o = out + (size_t)g * G::CS + y * 8 + x0;
+#pragma unroll
+        for (int z = 0; z < D; z++) {
+            float v[NXC];
+#pragma unroll
+            for (int e = 0; e < NXC; e++) {
+                double t = cz[z][e];
+                if constexpr (INV) t = t > 255.0 ? 255.0 : (t < 0.0 ? 0.0 : t);  // 3dDCT.cl:257-261
+                v[e] = (float)t;
+            }
+#pragma unroll
+            for (int e = 0; e < NXC; e += 4) *(float4*)(o + z * 64 + e) = make_float4(v[e], v[e + 1], v[e + 2], v[e + 3]);
+        }
+    }
+}
+
+int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st) {
+    const uint32_t per = (D == 8 ? DecGeom<8>::CPW : DecGeom<4>::CPW) * kWavesPerBlock;
+    const uint32_t blocks = (n_cubes + per - 1) / per;
+    if (!blocks) return 0;
+    if (D == 8) {
+        if (inverse) hipLaunchKernelGGL((cube_f32_kernel<8, true>), dim3(blocks), dim3(kBlock), 0, st, in, out, n_cubes);
+        else hipLaunchKernelGGL((cube_f32_kernel<8, false>), dim3(blocks), dim3(kBlock), 0, st, in, out, n_cubes);
+    } else {
+        if (inverse) hipLaunchKernelGGL((cube_f32_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, st, in, out, n_cubes);
+        else hipLaunchKernelGGL((cube_f32_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, st, in, out, n_cubes);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Fused stream -> raster decode (dct3d_decode_eg_dev; decoder.c:209-295 after the inflate): the

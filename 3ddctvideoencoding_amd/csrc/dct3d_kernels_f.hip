@@ -1,6 +1,6 @@
-// dct3d_kernels_f.hip -- floating-point-output kernels (fp64 internal arithmetic):
-//   * cube_f32_kernel<D, INV>: the reference-faithful drop-in (A): float cube-major in, float
-//     cube-major out -- DCT (3dDCT.cl:43-143) or inverse DCT clamped to [0,255] (3dDCT.cl:164-265).
+// dct3d_kernels_f.hip -- fp64 DCT output from the raster (fp64 internal arithmetic):
+//   (the drop-in (A) float kernel, cube_f32_kernel, shares the decode's geometry and lives in
+//   dct3d_kernels.hip)
 //   * fwd64_raster_kernel<D>: fp64 DCT coefficients straight from the u8 raster (the Java dctCoeff
 //     values, DCT.java:41-59) for the float-DCT parity output of dct3d_encode_stacks.
 // Same wave decomposition as dct3d_kernels.hip (8 cubes per wave, 8 lanes per cube, one
@@ -26,30 +26,6 @@ __device__ __forceinline__ void wave_sync_f() {
 }
 }  // namespace
 
-// Face layout (c, j) -> row layout (c, y): writer holds b[y][x'] (x' local), reader gets a[z][x].
-template <int D, int NB>
-__device__ __forceinline__ void face_to_row(const double (&b)[8][NB], double (&a)[D][8], int c, int j, char* wl) {
-    const int kz = (D == 8) ? j : (j >> 1);
-#pragma unroll
-    for (int qr = 0; qr < 4; qr++) {
-        const bool writer = (D == 8) || ((j & 1) == (qr >> 1));
-        if (writer) {
-            const int xl = (D == 8) ? 2 * qr : 2 * (qr & 1);
-#pragma unroll
-            for (int y = 0; y < 8; y++)
-                *(double2*)(wl + (c * 8 + y) * kSlotF + kz * 16) = make_double2(b[y][xl], b[y][xl + 1]);
-        }
-        wave_sync_f();
-#pragma unroll
-        for (int z = 0; z < D; z++) {
-            const double2 t = *(const double2*)(wl + (c * 8 + j) * kSlotF + z * 16);
-            a[z][2 * qr] = t.x;
-            a[z][2 * qr + 1] = t.y;
-        }
-        wave_sync_f();
-    }
-}
-
 // Row layout (c, y = j) -> face layout (c, j): writer holds a[kz][kx], reader gets b[y][kx'].
 template <int D, int NB>
 __device__ __forceinline__ void row_to_face(const double (&a)[D][8], double (&b)[8][NB], int c, int j, char* wl) {
@@ -71,74 +47,6 @@ __device__ __forceinline__ void row_to_face(const double (&a)[D][8], double (&b)
             }
         }
         wave_sync_f();
-    }
-}
-
-template <int D, bool INV>
-__global__ __launch_bounds__(256) void cube_f32_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                        uint32_t n_cubes) {
-    constexpr int CS = 64 * D;
-    constexpr int NB = (D == 8) ? 8 : 4;
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlockF * kWaveLdsF];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int c = lane >> 3, j = lane & 7;
-    char* wl = lds + wave * kWaveLdsF;
-    const uint32_t g = (blockIdx.x * kWavesPerBlockF + wave) * 8 + c;
-    const bool valid = g < n_cubes;
-    const int kz = (D == 8) ? j : (j >> 1);
-    const int x0 = (D == 8) ? 0 : (j & 1) * 4;
-
-    // face layout: (y, x0 .. x0+NB-1) of plane kz
-    double b[8][NB];
-#pragma unroll
-    for (int y = 0; y < 8; y++)
-#pragma unroll
-        for (int x = 0; x < NB; x += 4) {
-            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (valid) v = *(const float4*)(in + (size_t)g * CS + kz * 64 + y * 8 + x0 + x);
-            b[y][x] = v.x; b[y][x + 1] = v.y; b[y][x + 2] = v.z; b[y][x + 3] = v.w;
-        }
-#pragma unroll
-    for (int x = 0; x < NB; x++) {
-        double col[8];
-#pragma unroll
-        for (int y = 0; y < 8; y++) col[y] = b[y][x];
-        if constexpr (INV) idct8(col);
-        else fdct8<false, false>(col, 0.0);
-#pragma unroll
-        for (int y = 0; y < 8; y++) b[y][x] = col[y];
-    }
-    double a[D][8];
-    face_to_row<D, NB>(b, a, c, j, wl);
-#pragma unroll
-    for (int z = 0; z < D; z++) {
-        if constexpr (INV) idct8(a[z]);
-        else fdct8<false, false>(a[z], 0.0);
-    }
-#pragma unroll
-    for (int x = 0; x < 8; x++) {
-        double col[D];
-#pragma unroll
-        for (int z = 0; z < D; z++) col[z] = a[z][x];
-        if constexpr (INV) idctN<D>(col);
-        else fdctN<D, false, false>(col, 0.0);
-#pragma unroll
-        for (int z = 0; z < D; z++) a[z][x] = col[z];
-    }
-    if (valid) {
-#pragma unroll
-        for (int z = 0; z < D; z++) {
-            float v[8];
-#pragma unroll
-            for (int x = 0; x < 8; x++) {
-                double t = a[z][x];
-                if constexpr (INV) t = t > 255.0 ? 255.0 : (t < 0.0 ? 0.0 : t);  // 3dDCT.cl:257-261
-                v[x] = (float)t;
-            }
-            float* o = out + (size_t)g * CS + z * 64 + j * 8;
-            *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
-            *(float4*)(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-        }
     }
 }
 
@@ -204,19 +112,6 @@ __global__ __launch_bounds__(256) void fwd64_raster_kernel(Fwd64Params P) {
 #pragma unroll
             for (int x = 0; x < NB; x += 2) *(double2*)(o + y * 8 + x) = make_double2(b[y][x], b[y][x + 1]);
     }
-}
-
-int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st) {
-    const uint32_t blocks = (n_cubes + 31) / 32;
-    if (!blocks) return 0;
-    if (D == 8) {
-        if (inverse) hipLaunchKernelGGL((cube_f32_kernel<8, true>), dim3(blocks), dim3(256), 0, st, in, out, n_cubes);
-        else hipLaunchKernelGGL((cube_f32_kernel<8, false>), dim3(blocks), dim3(256), 0, st, in, out, n_cubes);
-    } else {
-        if (inverse) hipLaunchKernelGGL((cube_f32_kernel<4, true>), dim3(blocks), dim3(256), 0, st, in, out, n_cubes);
-        else hipLaunchKernelGGL((cube_f32_kernel<4, false>), dim3(blocks), dim3(256), 0, st, in, out, n_cubes);
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st) {

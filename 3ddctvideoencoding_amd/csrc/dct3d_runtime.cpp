@@ -282,12 +282,12 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
     st->n_timed = c->n_timed;
     st->kernel_ms_total = c->kernel_ms;
     st->fixup_ms_total = c->fixup_ms;
+    st->n_units = c->last_units;
     if (!c->last_valid) return DCT3D_OK;
     uint32_t cnt[4] = {0, 0, 0, 0};
     if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
-    st->n_units = c->last_units;
     st->n_flagged = cnt[0];
     st->n_overflow_cubes = cnt[1];
     return DCT3D_OK;
@@ -606,16 +606,31 @@ int dct3d_decode_stacks(dct3d_ctx* c, const int32_t* q, int w, int h, int n_stac
 }
 
 // ---- drop-in (A): float cube-major <-> float cube-major --------------------------------------
-int dct3d_forward_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* d_out) {
+// one launch of the float kernel, timed like the fused kernels when profiling is on (no fixup:
+// the second event pair brackets nothing)
+static int cube_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* d_out, bool inverse) {
     if (!c || (n_cubes && (!d_in || !d_out)) || n_cubes >= (1ull << 31) / 8) return DCT3D_EINVAL;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    return launch_cube_f32(c->bd, false, d_in, d_out, (uint32_t)n_cubes, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
+    if (!n_cubes) return DCT3D_OK;
+    hipEvent_t* ev = timing_slot(c);
+    if (ev) (void)hipEventRecord(ev[0], c->stream);
+    if (launch_cube_f32(c->bd, inverse, d_in, d_out, (uint32_t)n_cubes, c->stream)) return DCT3D_EKERNEL;
+    if (ev) {
+        (void)hipEventRecord(ev[1], c->stream);
+        (void)hipEventRecord(ev[2], c->stream);
+        (void)hipEventRecord(ev[3], c->stream);
+    }
+    c->last_units = n_cubes * (uint64_t)c->plan.cs;
+    c->last_valid = false;  // no flag counters for the float path
+    return DCT3D_OK;
+}
+
+int dct3d_forward_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* d_out) {
+    return cube_f32_dev(c, d_in, n_cubes, d_out, false);
 }
 
 int dct3d_inverse_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* d_out) {
-    if (!c || (n_cubes && (!d_in || !d_out)) || n_cubes >= (1ull << 31) / 8) return DCT3D_EINVAL;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    return launch_cube_f32(c->bd, true, d_in, d_out, (uint32_t)n_cubes, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
+    return cube_f32_dev(c, d_in, n_cubes, d_out, true);
 }
 
 static int cube_f32_host(dct3d_ctx* c, const float* in, size_t n_cubes, float* out, bool inverse) {

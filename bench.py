@@ -39,7 +39,31 @@ CONFIGS = {
     "c7_encode_eg_1080p": (1920, 1080, 8, 128, "encode_eg"),
     # decode from the Exp-Golomb stream: EG decode + dequantise + IDCT per step
     "c8_decode_eg_1080p": (1920, 1080, 8, 128, "decode_eg"),
+    # drop-in (A), the reference's own device block (encoder.c:231-276 / decoder.c:246-292): float
+    # cube-major in -> float cube-major out, DCT / IDCT + clamp, fp64 internal
+    "c9_forward_f32_1080p": (1920, 1080, 8, 128, "forward_f32"),
+    "c10_inverse_f32_1080p": (1920, 1080, 8, 128, "inverse_f32"),
 }
+
+# what one step computes, per direction (the headline metric is BASELINE.json's, config c2)
+WHAT = {
+    "encode": "forward 3D DCT + quantise",
+    "decode": "dequantise + inverse 3D DCT",
+    "encode_eg": "forward 3D DCT + quantise + diagonal order + Exp-Golomb stream",
+    "decode_eg": "Exp-Golomb decode + dequantise + inverse 3D DCT",
+    "forward_f32": "drop-in (A) forward 3D DCT, f32 cube-major in/out",
+    "inverse_f32": "drop-in (A) inverse 3D DCT + clamp, f32 cube-major in/out",
+}
+HEADLINE_METRIC = "8×8×8 cubes/s (encode DCT+quant) on 1080p×8-frame stacks; % HBM roofline at 1/2/4/8 GPUs"
+
+
+def metric_name(direction: str, depth: int) -> str:
+    """BASELINE.json's metric for the encode configs at depth 8; the same form, naming what is timed,
+    for the other configs (they are parity / coverage lines, not the headline)."""
+    if direction == "encode" and depth == 8:
+        return HEADLINE_METRIC
+    unit = "8×8×8" if depth == 8 else "8×8×4"
+    return f"{unit} cubes/s ({WHAT[direction]}) on 1080p×{depth}-frame stacks; % HBM roofline"
 
 
 def parse():
@@ -213,6 +237,23 @@ def main():
 
         def step():
             eg_info["bits"] = ctx.encode_eg_dev(frames, width, height, stacks, eg_out, eg_cap)  # synchronises
+    elif direction in ("forward_f32", "inverse_f32"):
+        nby, nbx = height // 8, width // 8
+        if direction == "forward_f32":  # readCubes (encoder.c:29-41): u8 raster -> float cube-major
+            f_in = (frames.view(stacks, depth, nby, 8, nbx, 8).permute(0, 2, 4, 1, 3, 5)
+                    .to(torch.float32).contiguous().view(-1))
+        else:  # applyDequantization (decoder.c:48-59) of the encoder's output, float cube-major
+            ctx.encode_stacks_dev(frames, width, height, stacks, q)
+            kk = torch.arange(cs, device="cuda")
+            steps = torch.clamp(5 * (kk % 8 + (kk // 8) % 8 + kk // 64), min=1).to(torch.float32)
+            f_in = (q.view(n_cubes, cs).to(torch.float32) * steps).view(-1)
+        del q
+        q = None
+        f_out = torch.empty_like(f_in)
+        run = ctx.forward_f32_dev if direction == "forward_f32" else ctx.inverse_f32_dev
+
+        def step():
+            run(f_in, n_cubes, f_out)
     else:
         def step():
             ctx.encode_stacks_dev(frames, width, height, stacks, q)
@@ -250,6 +291,8 @@ def main():
     ms_per_step = elapsed * 1e3 / a.steps
     value = total_cubes * a.steps / elapsed
     bytes_per_cube = cs * (1 + 4)  # u8 in + int32 out (encode) / int32 in + u8 out (decode)
+    if direction in ("forward_f32", "inverse_f32"):
+        bytes_per_cube = cs * (4 + 4)  # f32 in + f32 out (4,096 B per cube)
     fused = direction == "encode_eg" and not a.eg_two_step
     if fused:  # u8 in + the cube's share of the coded stream, lane bit counts and segment totals out
         bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes + (64 * 2 + 4) / 8
@@ -261,10 +304,12 @@ def main():
         bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes
     kname = ("decode_eg_kernel" if fused_dec else "decode_kernel") if direction in ("decode", "decode_eg") else (
         "encode_eg_kernel" if fused else "encode_kernel")
+    if direction in ("forward_f32", "inverse_f32"):
+        kname = "cube_f32_kernel"
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
-        "metric": "8×8×8 cubes/s (encode DCT+quant) on 1080p×8-frame stacks; % HBM roofline at 1/2/4/8 GPUs",
+        "metric": metric_name(direction, depth),
         "value": value,
         "unit": "cubes/s",
         "n_gpus": world,
@@ -274,11 +319,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64" if direction in ("decode", "decode_eg") else "f32",
+        "dtype": "f64" if direction in ("decode", "decode_eg", "forward_f32", "inverse_f32") else "f32",
         "data": "synthetic",
         "config": {
             "workload": f"{width}x{height} grayscale, {depth}-frame stacks, "
-                        f"{ {'encode': 'forward 3D DCT + quantise', 'decode': 'dequantise + inverse 3D DCT', 'encode_eg': 'forward 3D DCT + quantise + diagonal order + Exp-Golomb stream', 'decode_eg': 'Exp-Golomb decode + dequantise + inverse 3D DCT'}[direction] }"
+                        f"{WHAT[direction]}"
                         f" ({unit_name} cubes), {stacks} device-resident stacks per GPU per step",
             "name": a.config,
             "stacks_per_gpu": stacks,
