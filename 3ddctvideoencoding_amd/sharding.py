@@ -46,3 +46,60 @@ def checksum(q) -> int:
     w = (np.arange(a.size, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) | np.uint64(1)
     with np.errstate(over="ignore"):
         return int(np.bitwise_xor.reduce(a * w) if a.size else 0)
+
+
+# ---- optional host-of-record distribution: timed apart from the hot path ----------
+# A job whose frames live on one GPU (rank 0) hands every rank its contiguous stack range and collects
+# the quantised cubes back in stack order.  Point-to-point sends over RCCL (xGMI between the GPUs of a
+# node; gloo on CPU), posted together with batch_isend_irecv so that rank 0 drives all its links at once.
+# Not part of the timed path: the bench's default step has no data-path collective (each rank generates
+# its own stacks), `bench.py --xgmi` times these two steps separately.
+def _p2p(ops):
+    import torch.distributed as dist
+
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def scatter_stacks(full, local, n_stacks: int, stack_numel: int, rank: int, world: int) -> None:
+    """Rank 0 sends rank r the flat elements of its stacks shard(n_stacks, world, r) from `full` (rank 0
+    only; any tensor with n_stacks * stack_numel elements); every rank receives its range into `local`
+    (rank 0 copies its own)."""
+    import torch.distributed as dist
+
+    first, count = shard(n_stacks, world, rank)
+    if local.numel() < count * stack_numel:
+        raise ValueError("local buffer too small for this rank's shard")
+    ops = []
+    if rank == 0:
+        flat = full.reshape(-1)
+        for r in range(1, world):
+            f, c = shard(n_stacks, world, r)
+            if c:
+                ops.append(dist.P2POp(dist.isend, flat[f * stack_numel:(f + c) * stack_numel], r))
+        if count:
+            local.reshape(-1)[:count * stack_numel].copy_(flat[first * stack_numel:(first + count) * stack_numel])
+    elif count:
+        ops.append(dist.P2POp(dist.irecv, local.reshape(-1)[:count * stack_numel], 0))
+    _p2p(ops)
+
+
+def gather_stacks(local, full, n_stacks: int, stack_numel: int, rank: int, world: int) -> None:
+    """The inverse of scatter_stacks: rank r sends the first shard-size elements of `local`; rank 0
+    receives every range into its place in `full` (stack order)."""
+    import torch.distributed as dist
+
+    first, count = shard(n_stacks, world, rank)
+    ops = []
+    if rank == 0:
+        flat = full.reshape(-1)
+        for r in range(1, world):
+            f, c = shard(n_stacks, world, r)
+            if c:
+                ops.append(dist.P2POp(dist.irecv, flat[f * stack_numel:(f + c) * stack_numel], r))
+        if count:
+            flat[first * stack_numel:(first + count) * stack_numel].copy_(local.reshape(-1)[:count * stack_numel])
+    elif count:
+        ops.append(dist.P2POp(dist.isend, local.reshape(-1)[:count * stack_numel], 0))
+    _p2p(ops)

@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ceiling", action="store_true")
+    ap.add_argument("--xgmi", action="store_true",
+                    help="N>1, encode configs: also time the optional host-of-record distribution (SURVEY.md §8e): "
+                         "rank 0 scatters every rank's u8 stacks and gathers the int32 cubes back over RCCL p2p "
+                         "(reported under 'xgmi', never part of 'value')")
     ap.add_argument("--eg-two-step", action="store_true",
                     help="c7 / c8: the int32 cube-major intermediate plus the stand-alone Exp-Golomb stage (A/B)")
     return ap.parse_args()
@@ -142,6 +146,51 @@ def measure_ceiling(ctx, torch, frames, q, reps):
         ms = e0.elapsed_time(e1) / reps
         out[name + "_GBs"] = n_px * bytes_per_px / (ms * 1e-3) / 1e9
     return out
+
+
+def xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height, rank, world):
+    """Optional host-of-record distribution, timed apart from the hot path: rank 0 holds every rank's
+    stacks (the same synthetic content each rank generated for itself), scatters them over RCCL p2p
+    (xGMI), then gathers the quantised cubes back in stack order.  Both directions are verified: the
+    received frames equal the rank's own, the gathered cube sums equal the senders'."""
+    n_all = world * stacks
+    stack_px = depth * height * width
+    stack_q = q.numel() // stacks
+    full = None
+    if rank == 0:
+        full = torch.empty((n_all * depth, height, width), dtype=torch.uint8, device="cuda")
+        ctx.fill_synthetic_dev(full, width, height, n_all * depth, frame0=0)
+    recv = torch.empty_like(frames)
+    torch.cuda.synchronize()
+
+    def timed(fn):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_sc = timed(lambda: sharding.scatter_stacks(full, recv, n_all, stack_px, rank, world))
+    ok = torch.tensor([1 if torch.equal(recv, frames) else 0], dtype=torch.int64, device="cuda")
+    del full, recv
+    gathered = torch.empty((n_all * stack_q,), dtype=torch.int32, device="cuda") if rank == 0 else None
+    t_ga = timed(lambda: sharding.gather_stacks(q, gathered, n_all, stack_q, rank, world))
+    sums = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
+    dist.all_gather(sums, q.sum(dtype=torch.int64).view(1))
+    if rank == 0:
+        g = gathered.view(world, -1)
+        for r in range(world):
+            if int(g[r].sum(dtype=torch.int64).item()) != int(sums[r].item()):
+                ok.zero_()
+    del gathered
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"scatter_s": t_sc, "scatter_GBs": n_all * stack_px / t_sc / 1e9,
+            "gather_s": t_ga, "gather_GBs": n_all * stack_q * 4 / t_ga / 1e9,
+            "bytes_note": "job totals (rank 0's own shard is a local copy)", "verified": bool(ok.item())}
 
 
 def main():
@@ -287,6 +336,9 @@ def main():
     ceiling = None if a.no_ceiling or q is None else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
     sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
     elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
+    xgmi = None
+    if a.xgmi and dist is not None and direction == "encode" and os.environ.get("DCT3D_BENCH_BACKEND", "nccl") == "nccl":
+        xgmi = xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height, rank, world)
 
     ms_per_step = elapsed * 1e3 / a.steps
     value = total_cubes * a.steps / elapsed
@@ -357,6 +409,8 @@ def main():
         "round_trip": round_trip,
         "cpu_baseline": None,
     }
+    if xgmi is not None:
+        res["xgmi"] = xgmi
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         try:
             res["cpu_baseline"] = cpu_baseline(width, height, depth, a.cpu_baseline_seconds, a.kind)

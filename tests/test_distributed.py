@@ -73,3 +73,43 @@ def test_checksum_order_sensitive():
     a = np.arange(1000, dtype=np.int32)
     assert sh.checksum(a) != sh.checksum(a[::-1].copy())
     assert sh.checksum(a) == sh.checksum(a.copy())
+
+
+def _xgmi_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    sh = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    n_stacks, numel = 7, 40          # ragged: shards of 3/2/2 stacks at world 3
+    full = torch.arange(n_stacks * numel, dtype=torch.int32) if rank == 0 else None
+    first, count = sh.shard(n_stacks, world, rank)
+    local = torch.full((max(count, 1) * numel,), -1, dtype=torch.int32)
+    sh.scatter_stacks(full, local, n_stacks, numel, rank, world)
+    ok = bool(torch.equal(local[:count * numel], torch.arange(first * numel, (first + count) * numel, dtype=torch.int32)))
+    # each rank transforms its shard (stand-in for the kernel), rank 0 gathers in stack order
+    local[:count * numel] = local[:count * numel] * 3 + rank
+    back = torch.zeros(n_stacks * numel, dtype=torch.int32) if rank == 0 else None
+    sh.gather_stacks(local, back, n_stacks, numel, rank, world)
+    flags = [None] * world if rank == 0 else None
+    dist.gather_object(ok, flags, dst=0)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "back.npy"), back.numpy())
+        np.save(os.path.join(out_dir, "ok.npy"), np.array(flags))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scatter_gather_stacks_gloo(tmp_path, world):
+    """The optional host-of-record distribution (bench.py --xgmi): p2p scatter of stack ranges from
+    rank 0 and the gather back in stack order, with ragged shards."""
+    mp.spawn(_xgmi_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    assert np.load(tmp_path / "ok.npy").all()
+    back = np.load(tmp_path / "back.npy")
+    sh = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    exp = np.arange(7 * 40, dtype=np.int32) * 3
+    for r in range(world):
+        f, c = sh.shard(7, world, r)
+        exp[f * 40:(f + c) * 40] += r
+    assert np.array_equal(back, exp)
