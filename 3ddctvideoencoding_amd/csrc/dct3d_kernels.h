@@ -141,7 +141,10 @@ int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipSt
 int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,
                       hipStream_t st);
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
-int launch_eg_sync(const EgDecParams& P, int iteration, hipStream_t st);
+// resolve (pass 0): each chunk's true parse is followed from the exit of chunk t - 1 until it meets a
+// pass-0 boundary of chunk t (in the block's LDS window); status[0] = 0: every chunk met, the pass-0 exits
+// and counts are final.  Otherwise (or without resolve) confirming passes (iteration 1) follow.
+int launch_eg_sync(const EgDecParams& P, int iteration, int resolve, hipStream_t st);
 int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
 int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mark pass + emit
 int launch_eg_mark(const EgDecParams& P, hipStream_t st);

@@ -892,16 +892,19 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.status = (uint64_t*)c->d_egd_status.p;
     D.mark = (uint64_t*)c->d_egd_mark.p;
     D.q = nullptr;
-    // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts; two passes
-    // are the usual total); at most n_chunks + 1 passes by induction from chunk 0
+    // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts and, resolving,
+    // usually proves every chunk in sync by itself; otherwise confirming passes follow); at most
+    // n_chunks + 1 passes by induction from chunk 0.  DCT3D_EG_NO_RESOLVE: always confirm (A/B, tests)
+    const char* no_resolve = getenv("DCT3D_EG_NO_RESOLVE");
+    const bool resolve = !no_resolve || !*no_resolve || !strcmp(no_resolve, "0");
     int cur = 0;
     for (uint64_t it = 0; it <= n_chunks + 1; it++) {
         if (hipMemsetAsync(c->d_egd_status.p, 0, 32, c->stream) != hipSuccess) return DCT3D_EDEVICE;
         D.exit_in = ex[cur];
         D.exit_out = ex[cur ^ 1];
-        if (launch_eg_sync(D, (int)(it < 2 ? it : 1), c->stream)) return DCT3D_EKERNEL;
+        if (launch_eg_sync(D, (int)(it < 2 ? it : 1), resolve, c->stream)) return DCT3D_EKERNEL;
         cur ^= 1;
-        if (it == 0) continue;
+        if (it == 0 && !resolve) continue;
         uint64_t changed = 0;
         if (hipMemcpyAsync(&changed, c->d_egd_status.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
