@@ -35,7 +35,7 @@ ABI_SYMBOLS = (
     "dct3d_reset_timers",
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
-    "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev",
+    "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
     "dct3d_eg_encode_dev", "dct3d_encode_eg", "dct3d_eg_fetch", "dct3d_diagonal_order",
     "dct3d_eg_decode_dev", "dct3d_decode_eg", "dct3d_encode_eg_dev", "dct3d_decode_eg_dev",
 )
@@ -98,6 +98,7 @@ def lib() -> C.CDLL:
             getattr(L, name).argtypes = [vp, vp, sz, vp]
         L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
         L.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
+        L.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
         L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
         L.dct3d_eg_encode_dev.argtypes = [vp, vp, u64, C.c_uint8, i32, vp, u64, C.POINTER(u64)]
         L.dct3d_encode_eg.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, C.POINTER(u64)]
@@ -275,6 +276,11 @@ class Context:
         _check(lib().dct3d_bandwidth_probe_dev(self._h, _tptr(d_in) if d_in is not None else None,
                                                _tptr(d_out) if d_out is not None else None, n_px, mode),
                "dct3d_bandwidth_probe_dev")
+
+    def encode_memonly_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q) -> None:
+        """Diagnostic: the encode's memory traffic without its compute (d_q is NOT a DCT)."""
+        _check(lib().dct3d_encode_memonly_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q)),
+               "dct3d_encode_memonly_dev")
 
     # ---- Exp-Golomb stage (SURVEY.md §8f #1) ----
     def eg_encode_dev(self, d_q, n_cubes: int, d_out, out_cap: int, carry_byte: int = 0, carry_bits: int = 0) -> int:

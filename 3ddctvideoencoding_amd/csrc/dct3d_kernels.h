@@ -83,6 +83,7 @@ struct Fwd64Params {
 int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st);
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
 int launch_encode(int D, const EncodeParams& P, hipStream_t st);
+int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st);  // diagnostic
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
 struct EgParams {
     const int32_t* q;          // cube-major quantised values

@@ -253,6 +253,54 @@ __device__ __forceinline__ void store16(void* p, const int4& v) {
     }
 }
 
+// Stage the wave's 8 quantised cubes through LDS (face-padded cube-major) and store them 1 KiB per
+// instruction (lane (c, j) holds qv[ky][kx'] of cube c, kz = j (8x8x8) / j >> 1 (8x8x4)).
+template <int D, bool NT>
+__device__ __forceinline__ void enc_stage_store(const EncodeParams& P, const int32_t (&qv)[8][(D == 8) ? 8 : 4],
+                                                char* wl, int lane, uint32_t cube0) {
+    constexpr int CS = 64 * D;
+    const int c = lane >> 3, j = lane & 7;
+    const int kz = (D == 8) ? j : (j >> 1);
+    constexpr int ROUNDS = 2;
+    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
+    constexpr int CHUNK_ITERS = CUBES_PER_ROUND * (CS / 4) / 64;  // 16-byte chunks per lane per round
+#pragma unroll
+    for (int rd = 0; rd < ROUNDS; rd++) {
+        if ((c / CUBES_PER_ROUND) == rd) {
+            const int cc = c % CUBES_PER_ROUND;
+            if constexpr (D == 8) {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+                    for (int h = 0; h < 2; h++)
+                        *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
+                            make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
+            } else {
+#pragma unroll
+                for (int ky = 0; ky < 8; ky++)
+                    *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
+                        make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
+            }
+        }
+        wave_lds_sync();
+        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
+        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
+#pragma unroll
+        for (int t = 0; t < CHUNK_ITERS; t++) {
+            const int q = t * 64 + lane;                 // 16-byte chunk within the round
+            const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
+            const int face = (q >> 4) % D;
+            const int w = q & 15;
+            if (rcube0 + cc < P.n_cubes) {
+                const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
+                store16<NT>(outb + (size_t)q * 16, v);
+            }
+        }
+        wave_lds_sync();
+    }
+
+}
+
 // Everything after the row loads, for the 8 cubes from cube0: statistics, transform, quantise +
 // certify, staged 1 KiB stores, uncertified coefficients to the flag list.
 template <int D, bool NT>
@@ -325,44 +373,7 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
     }
     if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
 
-    // ---- stage through LDS (face-padded cube-major) and store 1 KiB per instruction ----
-    constexpr int ROUNDS = 2;
-    constexpr int CUBES_PER_ROUND = 8 / ROUNDS;
-    constexpr int CHUNK_ITERS = CUBES_PER_ROUND * (CS / 4) / 64;  // 16-byte chunks per lane per round
-#pragma unroll
-    for (int rd = 0; rd < ROUNDS; rd++) {
-        if ((c / CUBES_PER_ROUND) == rd) {
-            const int cc = c % CUBES_PER_ROUND;
-            if constexpr (D == 8) {
-#pragma unroll
-                for (int ky = 0; ky < 8; ky++)
-#pragma unroll
-                    for (int h = 0; h < 2; h++)
-                        *(int4*)(wl + (cc * 8 + kz) * kFace + ky * 32 + h * 16) =
-                            make_int4(qv[ky][4 * h], qv[ky][4 * h + 1], qv[ky][4 * h + 2], qv[ky][4 * h + 3]);
-            } else {
-#pragma unroll
-                for (int ky = 0; ky < 8; ky++)
-                    *(int4*)(wl + (cc * 4 + kz) * kFace + ky * 32 + (j & 1) * 16) =
-                        make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
-            }
-        }
-        wave_lds_sync();
-        const uint32_t rcube0 = cube0 + rd * CUBES_PER_ROUND;
-        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
-#pragma unroll
-        for (int t = 0; t < CHUNK_ITERS; t++) {
-            const int q = t * 64 + lane;                 // 16-byte chunk within the round
-            const int cc = q / (CS / 4);                 // CS*4 bytes per cube = CS/4 chunks
-            const int face = (q >> 4) % D;
-            const int w = q & 15;
-            if (rcube0 + cc < P.n_cubes) {
-                const int4 v = *(const int4*)(wl + (cc * D + face) * kFace + w * 16);
-                store16<NT>(outb + (size_t)q * 16, v);
-            }
-        }
-        wave_lds_sync();
-    }
+    enc_stage_store<D, NT>(P, qv, wl, lane, cube0);
 
     // ---- !INL rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
     if (!INL && __builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
@@ -412,6 +423,27 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     uint2 raw[D];
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
     if (cube0 < P.n_cubes) encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), lane, cube0);  // wave-uniform
+}
+
+// DIAGNOSTIC (dct3d_encode_memonly_dev; the output is NOT a DCT): the encode's memory traffic alone --
+// the same row loads, the same LDS staging and 1 KiB NT stores of 16 KiB per wave -- with the
+// transform, quantisation and certification replaced by a few integer ops on the loaded bytes.  Its
+// rate is the ceiling the encode's own traffic reaches on this device (bench.py: ceiling).
+template <int D>
+__global__ __launch_bounds__(kBlock, 4) void encode_memonly_kernel(EncodeParams P) {
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
+    constexpr int NB = (D == 8) ? 8 : 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
+    uint2 raw[D];
+    load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);
+    if (cube0 >= P.n_cubes) return;
+    int32_t qv[8][NB];
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+        for (int x = 0; x < NB; x++) qv[ky][x] = (int32_t)((ky & 1 ? raw[x % D].y : raw[x % D].x) >> (ky * 3 % 24)) & 255;
+    enc_stage_store<D, true>(P, qv, lds + wave * enc_wave_lds<D>(), lane, cube0);
 }
 
 // =============================================================================================
@@ -1475,6 +1507,15 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     }
     if (D == 8) launch_enc_variant<8>(variant, P, st);
     else launch_enc_variant<4>(variant, P, st);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st) {
+    if (P.n_cubes == 0) return 0;
+    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
+    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (D == 8) hipLaunchKernelGGL((encode_memonly_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P);
+    else hipLaunchKernelGGL((encode_memonly_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -396,6 +396,25 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     return DCT3D_OK;
 }
 
+int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q) {
+    if (!c || (!d_raster && n_stacks) || (!d_q && n_stacks)) return DCT3D_EINVAL;
+    uint64_t n_cubes;
+    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
+    if (rc) return rc;
+    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+    EncodeParams P;
+    memset(&P, 0, sizeof(P));
+    P.raster = d_raster;
+    P.out = d_q;
+    P.n_cubes = (uint32_t)n_cubes;
+    P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
+    P.nbx = (uint32_t)(w / 8);
+    P.width = (uint32_t)w;
+    P.plane = (uint64_t)w * h;
+    P.stack_stride = P.plane * c->bd;
+    return launch_encode_memonly(c->bd, P, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
+}
+
 int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_stacks, uint8_t* d_raster) {
     if (!c || (!d_raster && n_stacks) || (!d_q && n_stacks)) return DCT3D_EINVAL;
     uint64_t n_cubes;

@@ -128,11 +128,27 @@ def pmc_traffic(config: str, kernel: str, depth: int):
     return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
 
 
-def measure_ceiling(ctx, torch, frames, q, reps):
+def measure_ceiling(ctx, torch, frames, q, reps, geom=None):
     """Achievable HBM rates on this device for the path's traffic mix, same buffers, same stream:
-    mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only."""
+    mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only.
+    geom = (width, height, stacks, bytes_per_cube) for encode configs: also the encode kernel's own
+    traffic without its compute (dct3d_encode_memonly_dev: same loads, LDS staging, NT stores)."""
     n_px = frames.numel() // 16 * 16
     out = {}
+    if geom is not None:
+        width, height, stacks, bpc = geom
+        ctx.encode_memonly_dev(frames, width, height, stacks, q)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            ctx.encode_memonly_dev(frames, width, height, stacks, q)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        n_cubes = q.numel() // (bpc // 5)
+        out["encode_memonly_ms"] = ms
+        out["encode_memonly_GBs"] = n_cubes * bpc / (ms * 1e-3) / 1e9
     for name, mode, bytes_per_px in (("mix_1r4w", 0, 5), ("copy", 1, 2), ("write", 2, 4), ("write_plain", 5, 4),
                                       ("read", 3, 1)):
         ctx.bandwidth_probe_dev(frames, q, n_px, mode)
@@ -333,7 +349,9 @@ def main():
                             "decode is pinned by tests/test_gpu_parity.py",
                       "max_abs_err": int(d.abs().max()), "mean_abs_err": float(d.abs().to(torch.float64).mean()),
                       "psnr_db": (10.0 * math.log10(255.0 ** 2 / mse)) if mse > 0 else None}
-    ceiling = None if a.no_ceiling or q is None else measure_ceiling(ctx, torch, frames, q, max(3, a.steps // 2))
+    ceiling = None if a.no_ceiling or q is None else measure_ceiling(
+        ctx, torch, frames, q, max(3, a.steps // 2),
+        geom=(width, height, stacks, cs * 5) if direction == "encode" else None)
     sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
     elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
     xgmi = None
@@ -351,6 +369,8 @@ def main():
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
     fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
     achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
+    if ceiling and "encode_memonly_GBs" in ceiling:  # the kernel against its own traffic without compute
+        ceiling["kernel_vs_memonly"] = achieved / ceiling["encode_memonly_GBs"]
     fused_dec = direction == "decode_eg" and not a.eg_two_step
     if fused_dec:  # the cube's share of the stream in, u8 out
         bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes

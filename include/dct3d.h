@@ -166,6 +166,13 @@ int dct3d_fill_synthetic_dev(dct3d_ctx *ctx, uint8_t *d_frames, int width, int h
  * write with plain (temporal) stores.  n_px % 16 == 0. */
 int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, size_t n_px, int mode);
 
+/* Memory-only twin of dct3d_encode_stacks_dev (bench support; d_q receives NOT a DCT): the encode
+ * kernel's row loads, LDS staging and 1 KiB non-temporal stores of the same cubes, without the
+ * transform, quantisation, certification or fixup.  Its rate is the ceiling the encode's own traffic
+ * reaches on this device. */
+int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
+                             int32_t *d_q);
+
 /* ---- Exp-Golomb stage on the device -----------------------------------------
  * Replaces applyExpGolombCoding (encoder.c:60-71) over expGolomb_writeValue (ExpGolomb.c:32-64) /
  * ExpGolombWriter.java:19-49: the signed order-0 Exp-Golomb stream of n_cubes consecutive cube-major
