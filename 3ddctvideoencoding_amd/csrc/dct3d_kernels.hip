@@ -301,11 +301,36 @@ __device__ __forceinline__ void enc_stage_store(const EncodeParams& P, const int
 
 }
 
+// The quantise/certify tables in LDS as {1/step_s, G_s, 0.5 - E_s, 0} (s = kx + ky + kz < 22), one copy
+// per block at a fixed LDS address (no base register to keep live across the transform): LDS reads
+// instead of three global loads per sum waited on after the transform.  EVERY wave writes the whole
+// table right after its row loads (identical bits, so the other waves' writes change nothing) and
+// reads only after its own writes (one wave's LDS operations complete in order).
+constexpr int kTabN = 24;
+__device__ __forceinline__ void enc_tables(const EncodeParams& P, float4* tab, int lane) {
+    if (lane < kTabN) tab[lane] = make_float4(P.tab_rstep[lane], P.tab_G[lane], 0.5f - P.tab_E[lane], 0.f);
+}
+// Row ky of the quantise loop uses sums sz + ky .. sz + ky + NB - 1: the window slides by one entry per
+// row, read at the row's start (the opaque sz keeps the reads there), so 2 NB table registers are live
+// instead of 2 NI.
+template <int NB, int NI>
+__device__ __forceinline__ void tab_window(const float4* tab, int& sz, int ky, float A, float (&rr)[NI],
+                                           float (&thr)[NI]) {
+    asm volatile("" : "+v"(sz));
+    const int lo = ky == 0 ? 0 : ky + NB - 1;
+#pragma unroll
+    for (int i = lo; i < ky + NB; i++) {
+        const float* t = (const float*)(tab + sz + i);
+        rr[i] = t[0];
+        thr[i] = __builtin_fmaf(-A, t[1], t[2]);
+    }
+}
+
 // Everything after the row loads, for the 8 cubes from cube0: statistics, transform, quantise +
 // certify, staged 1 KiB stores, uncertified coefficients to the flag list.
 template <int D, bool NT>
-__device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (&raw)[D], char* wl, int lane,
-                                            uint32_t cube0) {
+__device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (&raw)[D], char* wl,
+                                            const float4* tab, int lane, uint32_t cube0) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
     constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
@@ -328,16 +353,9 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
     forward_cube<D, NB>(a, m, c, j, wl, b);
 
     // ---- quantise + certify (thr_s = 0.5 - (A*G_s + E_s), dct3d_plan.cpp) ----
-    // The per-lane tables are re-read each iteration (an opaque zero keeps the compiler from
-    // hoisting ~45 loop-invariant registers out of the loop; the reads hit L1/L2).
+    // The per-lane tables are read row by row from the block's LDS copy (enc_tables, tab_window).
     int sz = so;
-    asm volatile("" : "+v"(sz));
     float rr[NI], thr[NI];
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-        rr[i] = P.tab_rstep[sz + i];
-        thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
-    }
     // Uncertified coefficients: 8x8x4 (INL) appends them to the flag list inside the row loop while
     // q is in registers -- its exact ties (the 4-point k = 2 row is +-1/2) flag a quarter of the
     // waves; 8x8x8 (flags in ~5 % of waves, registers at the 128 limit) re-derives them after the
@@ -348,6 +366,7 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         pin(b[ky]);
+        tab_window<NB, NI>(tab, sz, ky, A, rr, thr);
         bool f = false;
         float qq[NB];
 #pragma unroll
@@ -418,11 +437,14 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
 template <int D, bool NT, bool NTL = false>
 __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
+    __shared__ float4 s_tab[kTabN];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
     uint2 raw[D];
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
-    if (cube0 < P.n_cubes) encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), lane, cube0);  // wave-uniform
+    if (cube0 >= P.n_cubes) return;  // wave-uniform
+    enc_tables(P, s_tab, lane);
+    encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), s_tab, lane, cube0);
 }
 
 // DIAGNOSTIC (dct3d_encode_memonly_dev; the output is NOT a DCT): the encode's memory traffic alone --
@@ -592,6 +614,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     float b[8][NB];
     forward_cube<D, NB>(a, m, c, j, wl, b);
 
+    // (the tables stay in global memory here: the kernel's LDS is exactly a quarter of the CU's)
     int sz = so;
     asm volatile("" : "+v"(sz));
     float rr[NI], thr[NI];
