@@ -447,6 +447,226 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), s_tab, lane, cube0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Encode, 16 lanes per cube (8x8x8): the decode's geometry in the forward direction.  Lane (c, k, h)
+// of the wave's 4 cubes: c = (lane >> 5) * 2 + ((lane & 15) >> 3), k = lane & 7, h = (lane >> 4) & 1
+// (a cube's lanes are the permlane16 pairs (l, l ^ 16)).
+//   rows  a[r][x]: row y = k of frame z = 4h + r                           4 lines along x: pass X
+//   swap  of the pair's off-diagonal 4x4 blocks: x = 4h + e, z = r in a[r][e], z = 4 + r in a[r][4 + e]
+//                                                                          4 lines along z: pass Z
+//   LDS   (two y halves) -> lane (c, kz = k, h): b[y][e], x = 4h + e       4 lines along y: pass Y
+//   quantise coefficient (kz = k, ky, kx = 4h + e): s = k + 4h + ky + e
+// Per line these are exactly encode_kernel's butterflies, in the same pass order (X, Z, Y): the
+// values, and so the certification bounds, are identical.  32 floats per lane instead of 64, 4.5 KiB
+// of LDS per wave: more waves per CU to hide each wave's transform latency.
+constexpr int kE16CPW = 4;     // cubes per wave
+constexpr int kE16TZ = 144;    // transpose: kz stride (4 y x 16 B per h, 2 h, + 16 B: bank spread)
+constexpr int kE16TC = 8 * kE16TZ;
+constexpr int kE16SC = 8 * kFace;  // output staging: cube stride (faces of 256 + 16 B)
+constexpr int kE16Lds = 4 * kE16TC;
+static_assert(kE16Lds >= 2 * kE16SC, "two staged cubes per round");
+
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
+    constexpr int CS = 512;
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
+    __shared__ float4 s_tab[kTabN];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kE16CPW;
+    const int k = lane & 7, h = (lane >> 4) & 1;
+    const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+    uint2 raw[4];
+    if (valid) {
+        const uint32_t st = g / P.cubes_per_stack;
+        const uint32_t rr = g - st * P.cubes_per_stack;
+        const uint32_t by = rr / P.nbx, bx = rr - by * P.nbx;
+        const uint8_t* src = P.raster + (size_t)st * P.stack_stride + (size_t)(by * 8 + k) * P.width + bx * 8 +
+                             (size_t)(4 * h) * P.plane;
+#pragma unroll
+        for (int r = 0; r < 4; r++) raw[r] = *(const uint2*)(src + (size_t)r * P.plane);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) raw[r] = make_uint2(0u, 0u);
+    }
+    if (cube0 >= P.n_cubes) return;  // wave-uniform
+    enc_tables(P, s_tab, lane);
+    char* wl = lds + wave * kE16Lds;
+
+    // ---- statistics over the cube's 16 lanes: S, m, A (as cube_stats) ----
+    float a[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            a[r][e] = byte_of(raw[r].x, e);
+            a[r][e + 4] = byte_of(raw[r].y, e);
+        }
+    uint32_t S = 0, mx = 0u, mn = 0x7F800000u;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        S = __builtin_amdgcn_udot4(raw[r].x, 0x01010101u, S, false);
+        S = __builtin_amdgcn_udot4(raw[r].y, 0x01010101u, S, false);
+#pragma unroll
+        for (int x = 0; x < 8; x += 2) {
+            const uint32_t u0 = __float_as_uint(a[r][x]), u1 = __float_as_uint(a[r][x + 1]);
+            asm("v_max3_u32 %0, %1, %2, %3" : "=v"(mx) : "v"(mx), "v"(u0), "v"(u1));
+            asm("v_min3_u32 %0, %1, %2, %3" : "=v"(mn) : "v"(mn), "v"(u0), "v"(u1));
+        }
+    }
+#pragma unroll
+    for (int o = 1; o <= 16; o <<= 1) {
+        if (o == 8) continue;  // the cube's lanes: k bits (1, 2, 4) and h (16)
+        S += __shfl_xor(S, o, 64);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    }
+    const int m = (int)((S + CS / 2) / CS);
+    float A = fmaxf(__uint_as_float(mx) - (float)m, (float)m - __uint_as_float(mn));
+    asm volatile("" : "+v"(S), "+v"(A));
+
+    // ---- pass X (exact integer front, centring folded into X0) ----
+    const float dcsub = 8.0f * (float)m;
+    pin(a[0]);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        fdct8<true, true>(a[r], dcsub);
+        if (r + 1 < 4) pin2(a[r], a[r + 1]);
+        else pin(a[r]);
+    }
+    // ---- swap the off-diagonal 4x4 blocks of the lane pair: lines along z ----
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[r][e]), __float_as_uint(a[r][4 + e]),
+                                                             false, false);
+            a[r][e] = __uint_as_float((uint32_t)sw[0]);
+            a[r][4 + e] = __uint_as_float((uint32_t)sw[1]);
+        }
+    // ---- pass Z: line e (x = 4h + e) = a[0..3][e], a[0..3][4 + e] ----
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        float col[8];
+#pragma unroll
+        for (int z = 0; z < 4; z++) {
+            col[z] = a[z][e];
+            col[4 + z] = a[z][4 + e];
+        }
+        pin(col);
+        fdct8<false, false>(col, 0.f);
+        pin(col);
+#pragma unroll
+        for (int z = 0; z < 4; z++) {
+            a[z][e] = col[z];
+            a[z][4 + e] = col[4 + z];
+        }
+    }
+    // now coefficient kz of line e: a[kz][e] (kz < 4), a[kz - 4][4 + e]
+
+    // ---- LDS transpose in two y halves: lane (c, y = k, h) -> lane (c, kz = k, h) ----
+    float b[8][4];
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {
+        if ((k >> 2) == rd) {
+            char* dst = wl + c * kE16TC + h * 64 + (k & 3) * 16;
+#pragma unroll
+            for (int kz = 0; kz < 8; kz++) {
+                const float* v = kz < 4 ? &a[kz][0] : &a[kz - 4][4];
+                *(float4*)(dst + kz * kE16TZ) = make_float4(v[0], v[1], v[2], v[3]);
+            }
+        }
+        wave_lds_sync();
+        const char* src = wl + c * kE16TC + k * kE16TZ + h * 64;
+#pragma unroll
+        for (int yy = 0; yy < 4; yy++) {
+            const float4 t = *(const float4*)(src + yy * 16);
+            b[4 * rd + yy][0] = t.x; b[4 * rd + yy][1] = t.y; b[4 * rd + yy][2] = t.z; b[4 * rd + yy][3] = t.w;
+        }
+        wave_lds_sync();
+    }
+    // ---- pass Y ----
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        float col[8];
+#pragma unroll
+        for (int y = 0; y < 8; y++) col[y] = b[y][e];
+        pin(col);
+        fdct8<false, false>(col, 0.f);
+        pin(col);
+#pragma unroll
+        for (int y = 0; y < 8; y++) b[y][e] = col[y];
+    }
+
+    // ---- quantise + certify; uncertified coefficients appended while q is in registers ----
+    int sz = k + 4 * h;
+    float rr[11], thr[11];
+    int32_t qv[8][4];
+    int overflow = 0;
+#pragma unroll
+    for (int ky = 0; ky < 8; ky++) {
+        pin(b[ky]);
+        tab_window<4, 11>(s_tab, sz, ky, A, rr, thr);
+        bool f = false;
+        float qq[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            qq[e] = b[ky][e] * rr[ky + e];
+            const float n = __builtin_rintf(qq[e]);
+            f |= __builtin_fabsf(qq[e] - n) >= thr[ky + e];
+            qv[ky][e] = (int32_t)n;
+        }
+        if (__builtin_expect(f && valid, 0)) {
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if (__builtin_fabsf(qq[e] - __builtin_rintf(qq[e])) >= thr[ky + e]) {
+                    const uint32_t kk = (uint32_t)((k * 8 + ky) * 8 + 4 * h + e);
+                    const uint32_t idx = atomicAdd(&P.counters[0], 1u);
+                    if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + kk;
+                    else overflow = 1;
+                }
+        }
+        pin(qv[ky]);
+        asm volatile("" : "+v"(overflow));
+    }
+    if (k == 0 && h == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC
+
+    // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {
+        if ((lane >> 5) == rd) {
+            char* dst = wl + (c & 1) * kE16SC + k * kFace + h * 16;
+#pragma unroll
+            for (int ky = 0; ky < 8; ky++)
+                *(int4*)(dst + ky * 32) = make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
+        }
+        wave_lds_sync();
+        const uint32_t rcube0 = cube0 + 2 * rd;
+        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int q = t * 64 + lane;  // 16-byte chunk of the round's two cubes
+            const int cc = q >> 7, face = (q >> 4) & 7, w = q & 15;
+            if (rcube0 + cc < P.n_cubes) {
+                const int4 v = *(const int4*)(wl + cc * kE16SC + face * kFace + w * 16);
+                store16<NT>(outb + (size_t)q * 16, v);
+            }
+        }
+        wave_lds_sync();
+    }
+    // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
+    const unsigned long long ov = __ballot(overflow != 0);
+    if (__builtin_expect(ov != 0ull, 0)) {
+        const int base = (lane & 32) + (lane & 8);
+        const unsigned long long cmask = (0xFFull << base) | (0xFFull << (base + 16));
+        if (overflow && (int)__builtin_ctzll(ov & cmask) == lane) {
+            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
+        }
+    }
+}
+
 // DIAGNOSTIC (dct3d_encode_memonly_dev; the output is NOT a DCT): the encode's memory traffic alone --
 // the same row loads, the same LDS staging and 1 KiB NT stores of 16 KiB per wave -- with the
 // transform, quantisation and certification replaced by a few integer ops on the loaded bytes.  Its
@@ -1486,10 +1706,12 @@ int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, un
 // =============================================================================================
 // Launchers
 // =============================================================================================
-// Encode variants (DCT3D_ENC_VARIANT, test/bench knob): 0 plain stores, 1 non-temporal stores of the
-// int32 output (default), 2 non-temporal stores and loads (profiles/r01/encode_variant_sweep.txt).
+// Encode variants (DCT3D_ENC_VARIANT, test/bench knob): 8 lanes per cube (encode_kernel): 0 plain
+// stores, 1 non-temporal stores of the int32 output, 2 non-temporal stores and loads; 6: 16 lanes per
+// cube (encode16_kernel, 8x8x8 only), NT stores.  Defaults: 6 for 8x8x8 (ramp content 1.986 vs 1.998 ms,
+// uniform noise 2.52 vs 2.83 ms against variant 1), 1 for 8x8x4 (profiles/r01/encode_variant_sweep.txt).
 namespace {
-constexpr int kDefaultVariant = 1;
+constexpr int kDefaultVariant = -1;
 // Occupancy knob (DCT3D_*_LDS_PAD_KB): extra dynamic LDS per block limits the blocks per CU.  HBM3E
 // serves the encode's 1:4 read/write stream faster from fewer concurrent waves (tools/hbm_probe.hip:
 // 5.68 TB/s at 8 waves/CU against 5.36 at 32), but both kernels need the occupancy to hide their own
@@ -1511,8 +1733,15 @@ void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, hipStream_t 
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
 }
+template <bool NT>
+void launch_enc16(const EncodeParams& P, hipStream_t st) {
+    const uint32_t groups = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
+    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    hipLaunchKernelGGL((encode16_kernel<NT>), dim3(blocks), dim3(kBlock), 0, st, P);
+}
 template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
+    if (D == 8 && v == 6) return launch_enc16<true>(P, st);
     switch (v) {
         case 0: launch_enc_t<D, false>(P, st); break;
         case 2: launch_enc_t<D, true, true>(P, st); break;
@@ -1523,13 +1752,11 @@ void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
 
 int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
-    static int variant = -1;
-    if (variant < 0) {
-        const char* e = getenv("DCT3D_ENC_VARIANT");
-        variant = e ? atoi(e) : kDefaultVariant;
-    }
-    if (D == 8) launch_enc_variant<8>(variant, P, st);
-    else launch_enc_variant<4>(variant, P, st);
+    // read per launch (a getenv is ~100 ns against a ~2 ms launch): tests switch variants in-process
+    const char* e = getenv("DCT3D_ENC_VARIANT");
+    const int variant = e ? atoi(e) : kDefaultVariant;  // -1: the depth's default
+    if (D == 8) launch_enc_variant<8>(variant < 0 ? 6 : variant, P, st);
+    else launch_enc_variant<4>(variant < 0 ? 1 : variant, P, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

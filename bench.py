@@ -121,7 +121,7 @@ def pmc_traffic(config: str, kernel: str, depth: int):
     vals = {}
     for r in csv.DictReader(open(path)):
         name = r["kernel"]
-        if f"{kernel}<{depth}" in name and "fixup" not in name:
+        if (f"{kernel}<{depth}" in name or (kernel == "encode16_kernel" and f"{kernel}<" in name)) and "fixup" not in name:
             vals[r["counter"]] = float(r["avg_per_launch_raw"])
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None, None
@@ -378,6 +378,8 @@ def main():
         "encode_eg_kernel" if fused else "encode_kernel")
     if direction in ("forward_f32", "inverse_f32"):
         kname = "cube_f32_kernel"
+    if kname == "encode_kernel" and depth == 8 and os.environ.get("DCT3D_ENC_VARIANT", "6") == "6":
+        kname = "encode16_kernel"  # the 8x8x8 default: 16 lanes per cube (not templated on the depth)
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
