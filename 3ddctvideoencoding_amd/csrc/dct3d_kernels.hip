@@ -466,18 +466,8 @@ constexpr int kE16SC = 8 * kFace;  // output staging: cube stride (faces of 256 
 constexpr int kE16Lds = 4 * kE16TC;
 static_assert(kE16Lds >= 2 * kE16SC, "two staged cubes per round");
 
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
-    constexpr int CS = 512;
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
-    __shared__ float4 s_tab[kTabN];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kE16CPW;
-    const int k = lane & 7, h = (lane >> 4) & 1;
-    const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
-    const uint32_t g = cube0 + c;
-    const bool valid = g < P.n_cubes;
-    uint2 raw[4];
+// rows of the lane's cube (row y = k of frames 4h .. 4h + 3), zero past the end
+__device__ __forceinline__ void e16_load(const EncodeParams& P, uint32_t g, bool valid, int k, int h, uint2 (&raw)[4]) {
     if (valid) {
         const uint32_t st = g / P.cubes_per_stack;
         const uint32_t rr = g - st * P.cubes_per_stack;
@@ -490,10 +480,15 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
 #pragma unroll
         for (int r = 0; r < 4; r++) raw[r] = make_uint2(0u, 0u);
     }
-    if (cube0 >= P.n_cubes) return;  // wave-uniform
-    enc_tables(P, s_tab, lane);
-    char* wl = lds + wave * kE16Lds;
+}
 
+// Statistics, passes X / Z / Y, quantise + certify, exact DC.  Uncertified coefficients are appended
+// to the flag list; overflow = 1: the list is full, the cube goes to the whole-cube replay.
+__device__ __forceinline__ void e16_body(const EncodeParams& P, const uint2 (&raw)[4], char* wl, const float4* tab,
+                                         int lane, uint32_t g, bool valid, int32_t (&qv)[8][4], int& overflow) {
+    constexpr int CS = 512;
+    const int k = lane & 7, h = (lane >> 4) & 1;
+    const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
     // ---- statistics over the cube's 16 lanes: S, m, A (as cube_stats) ----
     float a[4][8];
 #pragma unroll
@@ -602,12 +597,11 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     // ---- quantise + certify; uncertified coefficients appended while q is in registers ----
     int sz = k + 4 * h;
     float rr[11], thr[11];
-    int32_t qv[8][4];
-    int overflow = 0;
+    overflow = 0;
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         pin(b[ky]);
-        tab_window<4, 11>(s_tab, sz, ky, A, rr, thr);
+        tab_window<4, 11>(tab, sz, ky, A, rr, thr);
         bool f = false;
         float qq[4];
 #pragma unroll
@@ -631,6 +625,27 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
         asm volatile("" : "+v"(overflow));
     }
     if (k == 0 && h == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
+    constexpr int CS = 512;
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
+    __shared__ float4 s_tab[kTabN];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kE16CPW;
+    const int k = lane & 7, h = (lane >> 4) & 1;
+    const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+    uint2 raw[4];
+    e16_load(P, g, valid, k, h, raw);
+    if (cube0 >= P.n_cubes) return;  // wave-uniform
+    enc_tables(P, s_tab, lane);
+    char* wl = lds + wave * kE16Lds;
+    int32_t qv[8][4];
+    int overflow;
+    e16_body(P, raw, wl, s_tab, lane, g, valid, qv, overflow);
 
     // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
 #pragma unroll
@@ -955,6 +970,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     if (lane == 0) E.seg_bits[wid] = tot;
 }
+
 
 // =============================================================================================
 // Fused decode (fp64, certified)
