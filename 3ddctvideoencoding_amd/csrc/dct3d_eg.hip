@@ -547,23 +547,15 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const uint64_t last = m0 + 64 < n_marks ? P.mark[m0 + 64] : P.status[1];  // wave-uniform
     const uint64_t w0 = first >> 5;
     const uint64_t span = (last >> 5) + 4 - w0;
-    const uint32_t nwin = (uint32_t)(span < kEmitWinWords ? span : kEmitWinWords);  // bounded on any input
+    const bool fits = span <= kEmitWinWords;  // wave-uniform
+    const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* wl = lds[wave];
     for (uint32_t i = lane; i < nwin; i += 64) wl[i] = stream_word(P, w0 + i);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int32_t v[kMarkVals];
-    {
-        WinReader r{wl, nwin, 0, 0, 0, 0, 0};
-        r.seek(rel_bit(my, w0 * 32));
-#pragma unroll
-        for (uint32_t i = 0; i < kMarkVals; i++) {
-            uint32_t code = 1u;
-            (void)r.get(code);  // the mark pass has validated the stream
-            v[i] = eg_value(code);
-        }
-    }
+    parse_values<kMarkVals>(P, wl, nwin, w0, fits, my, v);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -166,4 +166,32 @@ __device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader
     return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
 }
 
+// A consumer lane's N values from stream bit `my` (a mark: the stream is validated by the mark pass).
+// fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin)); else
+// the parse reads the stream in global memory -- a wave whose 2,048 values average more than the window
+// holds (|q| >= 2^13 nearly everywhere: never written by an encoder of 8-bit frames, but a valid stream).
+template <int N>
+__device__ __forceinline__ void parse_values(const EgDecParams& P, const uint32_t* win, uint32_t nwin, uint64_t w0,
+                                             bool fits, uint64_t my, int32_t (&v)[N]) {
+    if (fits) {
+        WinReader r{win, nwin, 0, 0, 0, 0, 0};
+        r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            uint32_t code = 1u;
+            (void)r.get(code);
+            v[i] = eg_value(code);
+        }
+    } else {
+        BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
+        r.seek(my);
+#pragma unroll 4
+        for (int i = 0; i < N; i++) {
+            uint32_t code = 1u;
+            (void)r.get(code);
+            v[i] = eg_value(code);
+        }
+    }
+}
+
 }  // namespace dct3d

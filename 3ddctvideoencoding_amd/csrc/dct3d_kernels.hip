@@ -1465,21 +1465,13 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     const uint64_t w0 = first >> 5;
     const uint64_t span = (last >> 5) + 4 - w0;
     constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,304 words >= 2,048 values x 27 bits
-    const uint32_t nwin = (uint32_t)(span < WIN ? span : WIN);  // bounded on any input
+    const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_values)
+    const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* win = (uint32_t*)wl;
     for (uint32_t i = lane; i < nwin; i += 64) win[i] = stream_word(E, w0 + i);
     wave_lds_sync();
     int32_t v[32];
-    {
-        WinReader r{win, nwin, 0, 0, 0, 0, 0};
-        r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
-#pragma unroll
-        for (int i = 0; i < 32; i++) {
-            uint32_t code = 1u;
-            (void)r.get(code);  // the mark pass has validated the stream
-            v[i] = eg_value(code);
-        }
-    }
+    parse_values<32>(E, win, nwin, w0, fits, my, v);
     wave_lds_sync();
     {
         const uint32_t c = lane / PARTS, part = lane % PARTS;

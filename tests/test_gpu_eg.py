@@ -199,3 +199,18 @@ def test_eg_decode_resolve_and_confirming_passes(pkg, oracle, gpu_ctx8, monkeypa
     data, nbits = _expected(oracle, pkg, q, 8)
     got, eb = _eg_decode(gpu_ctx8, data, q.shape[0])
     assert eb == nbits and np.array_equal(got, q)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_eg_decode_dense_long_codes(pkg, oracle, gpu_ctx8, gpu_ctx4, depth):
+    """Every value a 49..61-bit code: one consumer wave's 2,048 values span ~120 k bits, more than its
+    LDS window holds -- the window must not silently truncate the parse."""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    rng = np.random.default_rng(7 + depth)
+    n = 4096 // (64 * depth) * 3 + 1  # three waves' worth + a ragged cube
+    q = rng.integers(2**24, 2**30, size=(n, depth, 8, 8)) * rng.choice([-1, 1], size=(n, depth, 8, 8))
+    q = q.astype(np.int32)
+    q[0, 0, :2] = 0  # a few short codes among them
+    data, nbits = _expected(oracle, pkg, q, depth)
+    got, eb = _eg_decode(ctx, data, n)
+    assert eb == nbits and np.array_equal(got, q)

@@ -206,3 +206,19 @@ def test_fused_decode_truncated_and_corrupt(pkg, gpu_ctx8):
     with pytest.raises(pkg.Dct3dError) as e:
         _decode_fused(gpu_ctx8, bytes(bad), 128, 64, 2)
     assert e.value.code in (pkg.DCT3D_EINVAL, pkg.DCT3D_ENODATA)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_fused_decode_dense_long_codes(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth):
+    """Streams no encoder of 8-bit frames writes (|q| >= 2^24: 49..61-bit codes everywhere) decode to the
+    Java-semantics raster (out-of-range q: whole-cube replay) -- no silently truncated window."""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    rng = np.random.default_rng(11 + depth)
+    n = ctx.n_cubes(64, 48, 2)
+    q = rng.integers(2**24, 2**30, size=(n, depth, 8, 8)) * rng.choice([-1, 1], size=(n, depth, 8, 8))
+    q = q.astype(np.int32)
+    q[::3] = rng.integers(-20, 21, size=q[::3].shape)  # ordinary cubes between them
+    data, nbits = _expected(oracle, pkg, q, depth)
+    got, eb = _decode_fused(ctx, data, 64, 48, 2)
+    assert eb == nbits
+    assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
