@@ -161,6 +161,58 @@ struct WinReader {
     }
 };
 
+// A validated stream in an LDS window (the consumers after the mark pass): no bounds checks (a valid
+// parse stays inside the staged range, which carries 4 words of slack), the leading-zero count from the
+// top 32 bits (a valid code has < 32 leading zeros, and >= 33 bits are buffered after a refill).
+struct ValidWinReader {
+    const uint32_t* s;
+    uint32_t next;
+    uint64_t buf;
+    int avail;
+    uint32_t pos;
+    uint32_t pre;
+    __device__ __forceinline__ void seek(uint32_t p) {
+        pos = p;
+        const uint32_t k = p >> 5;
+        const int sh = (int)(p & 31);
+        buf = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
+        avail = 64 - sh;
+        next = k + 2;
+        pre = s[next];
+    }
+    __device__ __forceinline__ uint32_t get() {
+        if (avail <= 32) {
+            buf |= (uint64_t)pre << (32 - avail);
+            avail += 32;
+            pre = s[++next];
+        }
+        const int z = __clz((int)(uint32_t)(buf >> 32));
+        const int width = 2 * z + 1;
+        uint32_t code;
+        if (__builtin_expect(width <= avail, 1)) {
+            code = (uint32_t)(buf >> (64 - width));
+            buf <<= width;
+            avail -= width;
+            pos += (uint32_t)width;
+        } else {  // a code longer than the buffered bits (|v| >= 2^16)
+            const uint32_t k = pos >> 5;
+            const int sh = (int)(pos & 31);
+            const uint64_t hi = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
+            const uint64_t w = sh ? (hi | ((uint64_t)s[k + 2] >> (32 - sh))) : hi;
+            code = (uint32_t)(w >> (64 - width));
+            seek(pos + (uint32_t)width);
+        }
+        return code;
+    }
+};
+
+// signed value of a code (ExpGolombReader.java:52-62, as eg_value): code = 2v (v > 0) or 1 - 2v
+// (v <= 0), i.e. v = code >> 1, negated when the code is odd
+__device__ __forceinline__ int32_t eg_value_fast(uint32_t code) {
+    const int32_t m = -(int32_t)(code & 1u);
+    return ((int32_t)(code >> 1) ^ m) - m;
+}
+
 __device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader.java:52-62
     const uint32_t m = code - 1u;
     return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
@@ -174,14 +226,10 @@ template <int N>
 __device__ __forceinline__ void parse_values(const EgDecParams& P, const uint32_t* win, uint32_t nwin, uint64_t w0,
                                              bool fits, uint64_t my, int32_t (&v)[N]) {
     if (fits) {
-        WinReader r{win, nwin, 0, 0, 0, 0, 0};
+        ValidWinReader r{win, 0, 0, 0, 0, 0};
         r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
 #pragma unroll
-        for (int i = 0; i < N; i++) {
-            uint32_t code = 1u;
-            (void)r.get(code);
-            v[i] = eg_value(code);
-        }
+        for (int i = 0; i < N; i++) v[i] = eg_value_fast(r.get());
     } else {
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
         r.seek(my);
