@@ -77,7 +77,7 @@ struct BitReader {
     // one codeword: false when 32 zero bits come first (invalid); *code = the (z+1)-bit value
     __device__ __forceinline__ bool get(uint32_t& code) {
         refill();
-        const int z = buf ? __clzll((long long)buf) : 64;
+        const int z = __clz((int)(uint32_t)(buf >> 32));  // 32: the top 32 bits are zero (invalid)
         if (z >= 32) return false;
         const int width = 2 * z + 1;
         if (width <= avail) {
@@ -141,7 +141,7 @@ struct WinReader {
     __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
     __device__ __forceinline__ bool get(uint32_t& code) {
         refill();
-        const int z = buf ? __clzll((long long)buf) : 64;
+        const int z = __clz((int)(uint32_t)(buf >> 32));  // 32: the top 32 bits are zero (invalid)
         if (z >= 32) return false;
         const int width = 2 * z + 1;
         if (width <= avail) {
