@@ -808,7 +808,7 @@ __device__ __forceinline__ uint32_t eg_code16(uint32_t x, uint32_t& width) {
     const int32_t v = (int32_t)(int16_t)(uint16_t)x;
     const uint32_t ng = (uint32_t)(-v);
     const uint32_t code = ((ng << 1) ^ (uint32_t)((int32_t)ng >> 31)) + 1u;
-    width = 63u - 2u * (uint32_t)__clz((int)code);
+    width = 63u - 2u * (uint32_t)__builtin_clz(code);  // code >= 1: a plain v_ffbh_u32 (no zero case)
     return code;
 }
 
@@ -937,9 +937,11 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     const int cp = lane >> 3, part = lane & 7;
     const bool lvalid = cube0 + cp < P.n_cubes;
     const char* cb = wl + cp * CUBE_B;
-    uint32_t* dst = E.slot + (size_t)wid * E.seg_cap + lane;
+    // the segment's slot base is wave-uniform (scalar); each store adds a 32-bit lane offset
+    char* const seg = (char*)(E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap);
+    uint32_t dofs = (uint32_t)lane * 4u;  // byte offset of the lane's next word: (nw * 64 + lane) * 4
     uint64_t acc = 0;
-    uint32_t nb = 0, nw = 0;
+    uint32_t nb = 0;
     if (lvalid) {
 #pragma unroll 1
         for (int i0 = 0; i0 < VPL; i0 += 8) {
@@ -956,13 +958,14 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
                 nb += width;
                 if (nb >= 32u) {
                     nb -= 32u;
-                    dst[(size_t)nw * 64] = (uint32_t)(acc >> nb);
-                    nw++;
+                    *(uint32_t*)(seg + dofs) = (uint32_t)(acc >> nb);
+                    dofs += 256u;
                 }
             }
         }
-        if (nb) dst[(size_t)nw * 64] = (uint32_t)(acc << (32u - nb));
+        if (nb) *(uint32_t*)(seg + dofs) = (uint32_t)(acc << (32u - nb));
     }
+    const uint32_t nw = (dofs - (uint32_t)lane * 4u) >> 8;  // full words stored
     const uint32_t lbits = lvalid ? nw * 32u + nb : 0u;
     E.lane_bits[(size_t)wid * 64 + lane] = (uint16_t)lbits;
     uint32_t tot = lbits;
