@@ -821,9 +821,14 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     constexpr int CUBE_B = 2 * CS + 16;    // int16 cube-major staging per cube (+16 B: bank spread)
     static_assert(8 * CUBE_B <= enc_wave_lds<D>(), "int16 staging must fit the wave region");
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
-    __shared__ int rs_sum[kWavesPerBlock][kMaxGroupsDev];
-    __shared__ double rs_prod[kWavesPerBlock][kMaxGroupsDev];
+    // exact-replay scratch (kMaxGroupsDev sums + products per wave): 8x8x8 keeps it in the tail of the
+    // wave's region behind the int16 staging, so that the block fits a quarter of the CU's LDS together
+    // with the table copy; 8x8x4's region has no such room
+    constexpr int RS_B = kMaxGroupsDev * (4 + 8);
+    constexpr bool RS_TAIL = 8 * CUBE_B + RS_B <= enc_wave_lds<D>();
+    __shared__ __attribute__((aligned(16))) char rs_extra[RS_TAIL ? 16 : kWavesPerBlock * RS_B];
     __shared__ __attribute__((aligned(16))) uint16_t s_pos[CS];  // stream position -> byte offset in a cube
+    __shared__ float4 s_tab[kTabN];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t wid = blockIdx.x * kWavesPerBlock + wave;  // segment index
     const uint32_t cube0 = wid * kCubesPerWave;
@@ -832,7 +837,10 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     for (int i = threadIdx.x; i < CS; i += kBlock) s_pos[i] = (uint16_t)(2 * E.diag[i]);
     __syncthreads();
     if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
+    enc_tables(P, s_tab, lane);
     char* wl = lds + wave * enc_wave_lds<D>();
+    char* rs = RS_TAIL ? wl + 8 * CUBE_B : rs_extra + wave * RS_B;
+    static_assert((8 * CUBE_B) % 8 == 0 && RS_B % 8 == 0, "replay scratch alignment");
     const int c = lane >> 3, j = lane & 7;
     const int kz = (D == 8) ? j : (j >> 1);
     const int kx0 = (D == 8) ? 0 : (j & 1) * 4;
@@ -849,20 +857,14 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     float b[8][NB];
     forward_cube<D, NB>(a, m, c, j, wl, b);
 
-    // (the tables stay in global memory here: the kernel's LDS is exactly a quarter of the CU's)
     int sz = so;
-    asm volatile("" : "+v"(sz));
     float rr[NI], thr[NI];
-#pragma unroll
-    for (int i = 0; i < NI; i++) {
-        rr[i] = P.tab_rstep[sz + i];
-        thr[i] = __builtin_fmaf(-A, P.tab_G[sz + i], 0.5f - P.tab_E[sz + i]);
-    }
     int32_t qv[8][NB];
     uint32_t fm_lo = 0, fm_hi = 0;  // uncertified mask: bit ky*NB + x (64 bits for NB = 8)
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         pin(b[ky]);
+        tab_window<NB, NI>(s_tab, sz, ky, A, rr, thr);
         bool f = false;
         float qq[NB];
 #pragma unroll
@@ -919,7 +921,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
             const int sj = src & 7, sc = src >> 3;
             const int skz = (D == 8) ? sj : (sj >> 1), skx0 = (D == 8) ? 0 : (sj & 1) * 4;
             const uint32_t k = (uint32_t)((skz * 8 + bit / NB) * 8 + skx0 + bit % NB);
-            const int q = exact_coef<D>(R, cube0 + sc, k, lane, rs_sum[wave], rs_prod[wave]);
+            const int q = exact_coef<D>(R, cube0 + sc, k, lane, (int*)rs, (double*)(rs + kMaxGroupsDev * 4));
             if (lane == 0) *(int16_t*)(wl + sc * CUBE_B + 2 * k) = (int16_t)q;
             if (lane == src) {
                 if (fm_lo) fm_lo &= fm_lo - 1;
