@@ -9,6 +9,13 @@ namespace dct3d {
 
 constexpr int kMaxGroupsDev = 64;  // == kMaxGroups in dct3d_plan.h; one LDS slot per lane
 
+// n / d for n < 2^31 as one 32x32->64 multiply and a shift (Granlund-Montgomery: s = 31 + ceil(log2 d),
+// m = ceil(2^s / d) < 2^32 gives floor(n m / 2^s) = floor(n / d) for every n < 2^31); set_fast_div
+// (dct3d_runtime.cpp) fills m and s on the host
+struct FastDiv {
+    uint32_t m, s;
+};
+
 struct EncodeParams {
     const uint8_t* raster;
     int32_t* out;
@@ -16,6 +23,7 @@ struct EncodeParams {
     uint32_t g_base;           // first cube of this launch (global index; 0 unless a tail launch)
     uint32_t cubes_per_stack;
     uint32_t nbx;              // cubes per block-row
+    FastDiv div_cps, div_nbx;  // the two divisions of the cube -> raster address map
     uint32_t width;
     uint64_t plane;            // width * height
     uint64_t stack_stride;     // D * plane
@@ -47,6 +55,7 @@ struct DecodeParams {
     const int32_t* in;
     uint8_t* out;
     uint32_t n_cubes, cubes_per_stack, nbx, width;
+    FastDiv div_cps, div_nbx;
     uint32_t cube_base;        // decode_eg_kernel: first cube of this launch (a chunk of whole stacks)
     uint64_t plane, stack_stride;
     double dec_G, dec_E;

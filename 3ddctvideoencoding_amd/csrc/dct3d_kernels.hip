@@ -88,6 +88,9 @@ __device__ __forceinline__ void pin(T (&x)[N]) {
 
 __device__ __forceinline__ float byte_of(uint32_t w, int b) { return (float)((w >> (8 * b)) & 0xFFu); }
 
+// n / d by FastDiv (dct3d_kernels.h): exact for n < 2^31 (cube indices are < 2^28)
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (uint32_t)(((uint64_t)n * f.m) >> f.s); }
+
 // =============================================================================================
 // Fused encode
 // =============================================================================================
@@ -96,9 +99,9 @@ typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 template <int D, bool NTL = false>
 __device__ __forceinline__ void load_rows(const EncodeParams& P, uint32_t g, bool valid, int j, uint2 (&raw)[D]) {
     if (valid) {
-        const uint32_t s = g / P.cubes_per_stack;
+        const uint32_t s = fdiv(g, P.div_cps);
         const uint32_t r = g - s * P.cubes_per_stack;
-        const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
+        const uint32_t by = fdiv(r, P.div_nbx), bx = r - by * P.nbx;
         const uint8_t* src = P.raster + (size_t)s * P.stack_stride + (size_t)(by * 8 + j) * P.width + bx * 8;
 #pragma unroll
         for (int z = 0; z < D; z++) {
@@ -469,9 +472,9 @@ static_assert(kE16Lds >= 2 * kE16SC, "two staged cubes per round");
 // rows of the lane's cube (row y = k of frames 4h .. 4h + 3), zero past the end
 __device__ __forceinline__ void e16_load(const EncodeParams& P, uint32_t g, bool valid, int k, int h, uint2 (&raw)[4]) {
     if (valid) {
-        const uint32_t st = g / P.cubes_per_stack;
+        const uint32_t st = fdiv(g, P.div_cps);
         const uint32_t rr = g - st * P.cubes_per_stack;
-        const uint32_t by = rr / P.nbx, bx = rr - by * P.nbx;
+        const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
         const uint8_t* src = P.raster + (size_t)st * P.stack_stride + (size_t)(by * 8 + k) * P.width + bx * 8 +
                              (size_t)(4 * h) * P.plane;
 #pragma unroll
@@ -1276,9 +1279,9 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         }
     }
     if (valid) {
-        const uint32_t s = g / P.cubes_per_stack;
+        const uint32_t s = fdiv(g, P.div_cps);
         const uint32_t rr = g - s * P.cubes_per_stack;
-        const uint32_t by = rr / P.nbx, bx = rr - by * P.nbx;
+        const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
         uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + y) * P.width + bx * 8 + x0;
 #pragma unroll
         for (int z = 0; z < D; z++) {

@@ -95,6 +95,21 @@ static int diagonal_order(int bw, int bh, int bd, uint16_t* out) {
     return n;
 }
 
+// FastDiv of the kernel params (dct3d_kernels.h): s = 31 + ceil(log2 d), m = ceil(2^s / d)
+static FastDiv fast_div(uint32_t d) {
+    uint32_t l = 0;
+    while ((1ull << l) < d) l++;
+    FastDiv f;
+    f.s = 31 + l;
+    f.m = (uint32_t)(((1ull << f.s) + d - 1) / d);
+    return f;
+}
+template <class T>
+static void set_fast_div(T& P) {
+    P.div_cps = fast_div(P.cubes_per_stack);
+    P.div_nbx = fast_div(P.nbx);
+}
+
 extern "C" {
 
 int dct3d_abi_version(void) { return DCT3D_ABI_VERSION; }
@@ -356,6 +371,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.g_base = 0;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
+    set_fast_div(P);
     P.width = (uint32_t)w;
     P.plane = plane;
     P.stack_stride = plane * D;
@@ -409,6 +425,7 @@ int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h
     P.n_cubes = (uint32_t)n_cubes;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
+    set_fast_div(P);
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
     P.stack_stride = P.plane * c->bd;
@@ -435,6 +452,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     P.cube_base = 0;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
+    set_fast_div(P);
     P.width = (uint32_t)w;
     P.plane = plane;
     P.stack_stride = plane * D;
@@ -774,6 +792,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     P.g_base = 0;
     P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
     P.nbx = (uint32_t)(w / 8);
+    set_fast_div(P);
     P.width = (uint32_t)w;
     P.plane = plane;
     P.stack_stride = plane * D;
@@ -993,6 +1012,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     P.n_cubes = (uint32_t)((st0 + ns) * cps);
     P.cubes_per_stack = (uint32_t)cps;
     P.nbx = (uint32_t)(w / 8);
+    set_fast_div(P);
     P.width = (uint32_t)w;
     P.plane = plane;
     P.stack_stride = plane * D;
