@@ -291,16 +291,30 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
     const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
     const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
     uint32_t prev = 0, first = 0, last = 0;
-    for (uint32_t d = 0; d < ndst; d++) {
-        uint32_t cur;
-        if (d >= nsrc) cur = 0u;
-        else if (d < 4) cur = d == 0 ? pre[0] : d == 1 ? pre[1] : d == 2 ? pre[2] : pre[3];
-        else cur = src[(size_t)d * 64];
-        const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
-        prev = cur;
-        if (d == 0) first = v;
-        if (d == ndst - 1) last = v;
-        if (d != 0 && d != ndst - 1) P.out[w0 + d] = __builtin_bswap32(v);
+    uint32_t buf[4] = {pre[0], pre[1], pre[2], pre[3]};
+    for (uint32_t d0 = 0; d0 < ndst; d0 += 4) {
+        // rows d0 + 4 .. d0 + 7 in flight while rows d0 .. d0 + 3 are placed: a dense lane (the
+        // low-frequency part of a cube: up to 54 rows) waits one load round trip per 4 rows, not per row
+        uint32_t nxt[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t d = d0 + 4 + t;
+            nxt[t] = d < nsrc ? src[(size_t)d * 64] : 0u;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t d = d0 + t;
+            if (d < ndst) {
+                const uint32_t cur = d < nsrc ? buf[t] : 0u;
+                const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
+                prev = cur;
+                if (d == 0) first = v;
+                if (d == ndst - 1) last = v;
+                if (d != 0 && d != ndst - 1) P.out[w0 + d] = __builtin_bswap32(v);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) buf[t] = nxt[t];
     }
     const uint32_t nfirst = __shfl_down(first, 1, 64);
     if (next_shares) last |= nfirst;  // ndst == 1 only when r == 0 and lb == 32: never shared then
