@@ -505,8 +505,8 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const LdsBits L = stage_block_window(P, win);
     const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (t >= P.n_chunks) return;
-    uint64_t idx = P.off[t];
-    if (idx >= P.n_values) return;
+    const uint64_t idx0 = P.off[t];
+    if (idx0 >= P.n_values) return;
     // the converged exits are in exit_in (the host swaps the buffers after every pass)
     const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
     if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
@@ -515,20 +515,28 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t limit = rel_bit(P.limit_bit, base);
     WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
     r.seek(rel_bit(s, base));
-    uint32_t code;
-    while (idx < P.n_values && r.pos < end) {
+    // chunk-relative 32-bit value count i (value idx0 + i): the 64-bit index arithmetic per step was a
+    // large part of the pass.  A chunk holds at most ~kChunkBits + 64 codes, so rem below never binds
+    // unless the wanted values end inside this chunk.
+    const uint64_t rem64 = P.n_values - idx0;
+    const uint32_t rem = (uint32_t)min(rem64, (uint64_t)(2 * kChunkBits));
+    const bool ends_here = rem64 <= 2 * kChunkBits;
+    const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
+    uint64_t* const mk = P.mark + (idx0 / kMarkVals);  // mark[(idx0 + i) / 32] = mk[(ph + i) / 32]
+    uint32_t i = 0, code;
+    while (i < rem && r.pos < end) {
         const uint32_t p0 = r.pos;
         if (p0 >= limit) {  // ran out of bits
             atomicOr((unsigned int*)&P.status[2], 2u);
             return;
         }
-        const uint64_t room = min((uint64_t)min(end - p0, limit - p0), P.n_values - idx);
-        const uint32_t k = r.ones((uint32_t)min(room, (uint64_t)64));
-        if (k) {  // values idx .. idx + k - 1 are zeros at bits p0 .. p0 + k - 1
-            for (uint64_t m = (idx + kMarkVals - 1) & ~(uint64_t)(kMarkVals - 1); m < idx + k; m += kMarkVals)
-                P.mark[m / kMarkVals] = base + p0 + (m - idx);
-            idx += k;
-            if (idx == P.n_values) P.status[1] = base + r.pos;  // the bit after the last wanted value
+        const uint32_t room = min(min(end - p0, limit - p0), rem - i);
+        const uint32_t k = r.ones(min(room, 64u));
+        if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
+            for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
+                mk[(ph + j) / kMarkVals] = base + p0 + (j - i);
+            i += k;
+            if (ends_here && i == rem) P.status[1] = base + r.pos;  // the bit after the last wanted value
             continue;
         }
         if (!r.at_long_code()) continue;  // refill
@@ -537,8 +545,8 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
             atomicOr((unsigned int*)&P.status[2], (uint64_t)p0 + 32 <= limit && r.pos <= limit ? 1u : 2u);
             return;
         }
-        if ((idx & (kMarkVals - 1)) == 0) P.mark[idx / kMarkVals] = base + p0;
-        if (++idx == P.n_values) P.status[1] = base + r.pos;
+        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p0;
+        if (++i == rem && ends_here) P.status[1] = base + r.pos;
     }
 }
 
