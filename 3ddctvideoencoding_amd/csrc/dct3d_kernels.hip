@@ -1040,7 +1040,10 @@ __device__ __forceinline__ void dec_load_tile_p(const char* in, uint32_t n_cubes
     const char* inb = in + (size_t)cube0 * G::CS * 4;
     if (cube0 + G::CPW <= n_cubes) {  // wave-uniform: every cube of the tile exists
 #pragma unroll
-        for (int t = 0; t < 8; t++) v[t] = *(const int4*)(inb + (size_t)(t * 64 + lane) * 16);
+        for (int t = 0; t < 8; t++) {
+            const i32x4_t x = __builtin_nontemporal_load((const i32x4_t*)(inb + (size_t)(t * 64 + lane) * 16));
+            v[t] = make_int4(x.x, x.y, x.z, x.w);
+        }
     } else {
 #pragma unroll
         for (int t = 0; t < 8; t++) {
