@@ -186,21 +186,25 @@ struct ValidWinReader {
             avail += 32;
             pre = s[++next];
         }
-        const int z = __clz((int)(uint32_t)(buf >> 32));
+        const int z = __builtin_clz((uint32_t)(buf >> 32));  // a valid code: the top 32 bits are not 0
         const int width = 2 * z + 1;
-        uint32_t code;
-        if (__builtin_expect(width <= avail, 1)) {
-            code = (uint32_t)(buf >> (64 - width));
-            buf <<= width;
-            avail -= width;
-            pos += (uint32_t)width;
-        } else {  // a code longer than the buffered bits (|v| >= 2^16)
-            const uint32_t k = pos >> 5;
-            const int sh = (int)(pos & 31);
-            const uint64_t hi = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
-            const uint64_t w = sh ? (hi | ((uint64_t)s[k + 2] >> (32 - sh))) : hi;
-            code = (uint32_t)(w >> (64 - width));
-            seek(pos + (uint32_t)width);
+        const bool fits = width <= avail;
+        // the common case for every lane without a branch; a code longer than the buffered bits
+        // (|v| >= 2^16) is re-read after a wave-uniform test (no divergent if / else per code)
+        uint32_t code = (uint32_t)(buf >> (64 - width));
+        buf <<= width;
+        avail -= width;
+        pos += (uint32_t)width;
+        if (__builtin_expect(__ballot(!fits) != 0ull, 0)) {
+            if (!fits) {
+                const uint32_t p = pos - (uint32_t)width;
+                const uint32_t k = p >> 5;
+                const int sh = (int)(p & 31);
+                const uint64_t hi = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
+                const uint64_t w = sh ? (hi | ((uint64_t)s[k + 2] >> (32 - sh))) : hi;
+                code = (uint32_t)(w >> (64 - width));
+                seek(pos);
+            }
         }
         return code;
     }
