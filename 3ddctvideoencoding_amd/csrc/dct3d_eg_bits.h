@@ -141,21 +141,25 @@ struct WinReader {
     __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
     __device__ __forceinline__ bool get(uint32_t& code) {
         refill();
-        const int z = __clz((int)(uint32_t)(buf >> 32));  // 32: the top 32 bits are zero (invalid)
-        if (z >= 32) return false;
-        const int width = 2 * z + 1;
-        if (width <= avail) {
-            code = (uint32_t)(buf >> (64 - width));
-            buf <<= width;
-            avail -= width;
-            pos += (uint32_t)width;
-        } else {  // a long code straddling the buffer (|v| >= 2^16: never for quantised 8-bit content)
-            const uint32_t k = pos >> 5;
-            const int sh = (int)(pos & 31);
-            const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
-            const uint64_t w = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
-            code = (uint32_t)(w >> (64 - width));
-            seek(pos + (uint32_t)width);
+        const uint32_t hi32 = (uint32_t)(buf >> 32);
+        if (hi32 == 0u) return false;  // 32 zero bits: invalid
+        const int width = 2 * __builtin_clz(hi32) + 1;
+        const bool fits = width <= avail;
+        // the common case without a divergent if / else (as ValidWinReader)
+        code = (uint32_t)(buf >> (64 - width));
+        buf <<= width;
+        avail -= width;
+        pos += (uint32_t)width;
+        if (__builtin_expect(__ballot(!fits) != 0ull, 0)) {
+            if (!fits) {  // a long code straddling the buffer (|v| >= 2^16: never for quantised 8-bit content)
+                const uint32_t p = pos - (uint32_t)width;
+                const uint32_t k = p >> 5;
+                const int sh = (int)(p & 31);
+                const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+                const uint64_t w = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
+                code = (uint32_t)(w >> (64 - width));
+                seek(pos);
+            }
         }
         return true;
     }
