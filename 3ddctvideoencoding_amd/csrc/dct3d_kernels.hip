@@ -1756,7 +1756,8 @@ template <bool NT>
 void launch_enc16(const EncodeParams& P, hipStream_t st) {
     const uint32_t groups = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode16_kernel<NT>), dim3(blocks), dim3(kBlock), 0, st, P);
+    static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);  // occupancy knob (see lds_pad)
+    hipLaunchKernelGGL((encode16_kernel<NT>), dim3(blocks), dim3(kBlock), pad, st, P);
 }
 template <int D>
 void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
