@@ -630,7 +630,9 @@ __device__ __forceinline__ void e16_body(const EncodeParams& P, const uint2 (&ra
     if (k == 0 && h == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC
 }
 
-template <bool NT>
+// MEM (dct3d_encode_memonly_dev, DIAGNOSTIC: the output is NOT a DCT): the same loads, staging and
+// stores with the transform, quantisation and certification replaced by a few integer ops
+template <bool NT, bool MEM = false>
 __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
@@ -644,11 +646,18 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     uint2 raw[4];
     e16_load(P, g, valid, k, h, raw);
     if (cube0 >= P.n_cubes) return;  // wave-uniform
-    enc_tables(P, s_tab, lane);
     char* wl = lds + wave * kE16Lds;
     int32_t qv[8][4];
-    int overflow;
-    e16_body(P, raw, wl, s_tab, lane, g, valid, qv, overflow);
+    int overflow = 0;
+    if constexpr (MEM) {
+#pragma unroll
+        for (int ky = 0; ky < 8; ky++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) qv[ky][e] = (int32_t)(((ky & 1) ? raw[e].y : raw[e].x) >> (ky * 3 % 24)) & 255;
+    } else {
+        enc_tables(P, s_tab, lane);
+        e16_body(P, raw, wl, s_tab, lane, g, valid, qv, overflow);
+    }
 
     // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
 #pragma unroll
@@ -1782,6 +1791,13 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
 
 int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
+    const char* ev = getenv("DCT3D_ENC_VARIANT");
+    if (D == 8 && (!ev || atoi(ev) == 6 || atoi(ev) < 0)) {  // the twin of the default 16-lane kernel
+        const uint32_t groups16 = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
+        hipLaunchKernelGGL((encode16_kernel<true, true>), dim3((groups16 + kWavesPerBlock - 1) / kWavesPerBlock),
+                           dim3(kBlock), 0, st, P);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     if (D == 8) hipLaunchKernelGGL((encode_memonly_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P);
