@@ -1795,7 +1795,7 @@ int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st) {
     if (D == 8 && (!ev || atoi(ev) == 6 || atoi(ev) < 0)) {  // the twin of the default 16-lane kernel
         const uint32_t groups16 = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
         hipLaunchKernelGGL((encode16_kernel<true, true>), dim3((groups16 + kWavesPerBlock - 1) / kWavesPerBlock),
-                           dim3(kBlock), 0, st, P);
+                           dim3(kBlock), lds_pad("DCT3D_ENC_LDS_PAD_KB", 0), st, P);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
