@@ -268,14 +268,16 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
     const int lane = threadIdx.x & 63;
     const uint64_t s = (uint64_t)blockIdx.x * kEgWaves + (threadIdx.x >> 6);
     if (s >= P.n_cubes) return;
-    const uint32_t* src = slot + s * (uint64_t)seg_cap + lane;
+    // wave-uniform (scalar) bases with 32-bit lane offsets: the segment's slot and its first output word
+    const uint32_t* seg = slot + (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)s) * seg_cap;
     // independent loads, one round trip: the first 4 rows unconditionally (a slot has >= 27 rows;
     // words past a lane's last one are never used), its bit count, the segment offset
     uint32_t pre[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) pre[t] = src[t * 64];
+    for (int t = 0; t < 4; t++) pre[t] = seg[t * 64 + lane];
     const uint32_t lb = lane_bits[s * 64 + lane];
     const uint64_t base = P.off[s];
+    uint32_t* const outs = P.out + (base >> 5);
     const uint32_t nsrc = (lb + 31) >> 5;
     uint32_t incl = lb;
 #pragma unroll
@@ -286,6 +288,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
     const uint64_t start = base + (incl - lb);
     const uint32_t r = (uint32_t)(start & 31);
     const uint64_t w0 = start >> 5;
+    const uint32_t wrel = (uint32_t)(w0 - (base >> 5));  // < 54 * 64 words into the segment
     const uint32_t ndst = lb ? (uint32_t)(((start + lb - 1) >> 5) - w0 + 1) : 0u;
     const uint32_t nlb = __shfl_down(lb, 1, 64);
     const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 #pragma unroll
         for (int t = 0; t < 4; t++) {
             const uint32_t d = d0 + 4 + t;
-            nxt[t] = d < nsrc ? src[(size_t)d * 64] : 0u;
+            nxt[t] = d < nsrc ? seg[d * 64u + (uint32_t)lane] : 0u;
         }
 #pragma unroll
         for (int t = 0; t < 4; t++) {
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
                 prev = cur;
                 if (d == 0) first = v;
                 if (d == ndst - 1) last = v;
-                if (d != 0 && d != ndst - 1) P.out[w0 + d] = __builtin_bswap32(v);
+                if (d != 0 && d != ndst - 1) outs[wrel + d] = __builtin_bswap32(v);
             }
         }
 #pragma unroll

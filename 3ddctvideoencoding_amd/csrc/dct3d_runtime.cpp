@@ -171,7 +171,9 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         delete c;
         return DCT3D_EINVAL;
     }
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    // the context's own stream is a blocking stream: ordered with the legacy default stream, so device
+    // buffers a caller fills or reads there (e.g. a framework's default stream) need no extra sync
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamDefault) != hipSuccess) {
         delete c;
         return DCT3D_EDEVICE;
     }

@@ -19,7 +19,8 @@
  *     thread per context (a context is not thread-safe);
  *   - host-pointer entry points are synchronous on return (the reference's blocking
  *     clEnqueueWrite/ReadBuffer, encoder.c:231,276); *_dev entry points take device pointers and
- *     are asynchronous on the context stream (use dct3d_synchronize);
+ *     are asynchronous on the context stream (use dct3d_synchronize).  The context's own stream is a
+ *     blocking stream (ordered with the legacy default stream); dct3d_ctx_set_stream selects another;
  *   - frame width must be a multiple of the block width and height of the block height
  *     (1080 = 135 * 8); the reference silently overruns otherwise, this library returns
  *     DCT3D_EINVAL.

@@ -153,6 +153,7 @@ def _decode_two_step(ctx, data: bytes, w, h, stacks, start_bit=0):
     eb = ctx.eg_decode_dev(d, len(data), start_bit, n, q)
     out = torch.empty((stacks * ctx.bd, h, w), dtype=torch.uint8, device="cuda")
     ctx.decode_stacks_dev(q, w, h, stacks, out)
+    ctx.synchronize()  # *_dev calls are asynchronous on the context stream
     return out.cpu().numpy(), eb
 
 
