@@ -1,8 +1,12 @@
 // dct3d_kernels.hip -- CDNA4 (gfx950) kernels of the 3D-DCT hot path.
 //
-// Work decomposition (all transform kernels): one wave64 owns 8 cubes, 8 lanes per cube.
+// Work decomposition.  The 8x8x4 encode (and the 8-lane 8x8x8 form, variant 1): one wave64 owns 8
+// cubes, 8 lanes per cube.
 //   "row layout"  lane (c, y)        holds a[z][x]   (D x 8 values): the cube's row y of every frame
 //   "face layout" lane (c, kz[,h])   holds b[y][x]   (8 x 8 or 8 x 4 values): one z-face (or half)
+// The default 8x8x8 encode (encode16_kernel), the decode and the float drop-ins: 16 lanes per cube
+// (2 D lanes for 8x8x4 decode), 32 values per lane, the permlane16 pair (l, l ^ 16) splitting each cube
+// (DecGeom; encode16_kernel's comment has its three layouts).
 // Two of the three separable 8-point passes run in registers in one layout, the third in the other;
 // the single layout change is a wave-private LDS transpose (no workgroup barrier: one wave writes
 // and reads its own region, LDS ops of a wave execute in order).  Cube-major int32 / fp64 traffic is
