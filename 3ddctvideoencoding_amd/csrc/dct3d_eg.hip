@@ -657,6 +657,12 @@ int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* l
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_eg_stitch(const EgParams& P, hipStream_t st) {
+    if (P.n_cubes == 0) return 0;
+    hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_eg_mark(const EgDecParams& P, hipStream_t st) {
     if (P.n_chunks == 0) return 0;
     hipLaunchKernelGGL(eg_mark_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);

@@ -141,11 +141,24 @@ struct EgFusedParams {
                                // first bit at bit 31 of its word 0
     uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
     uint16_t* lane_bits;       // [n_seg * 64] bits coded by each lane
-    uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
+    uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input; single pass: the stitch's)
+    // single pass (encode_eg_kernel<D, true>): each wave places its segment in the stream itself,
+    // its offset from a decoupled look-back over the preceding segments (no slot, scan or compaction)
+    uint64_t* seg_state;       // [n_seg] look-back words, zeroed per call: bit 63 inclusive prefix,
+                               // bit 62 aggregate (bits 0..61 the value), both = this segment gave up
+    uint64_t* seg_off;         // [n_seg] stream bit offset of each segment (carry included)
+    uint32_t* head;            // [n_seg] first / last output word of each segment (eg_stitch_kernel)
+    uint32_t* tail;
+    uint32_t* out;             // output words (memory byte order)
+    uint64_t out_cap_words;
+    uint64_t* status;          // [0] total bits (carry included), [1] 1: capacity, 4: look-back gave up
+    uint32_t carry_bits;
 };
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
-int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st);
+// single_pass: the look-back variant (E.seg_state zeroed; eg_stitch afterwards, no compaction)
+int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, bool single_pass, hipStream_t st);
+int launch_eg_stitch(const EgParams& P, hipStream_t st);
 // scan of the segment bits + the lanes' words concatenated into the stream + stitch (P.n_cubes =
 // segments, P.bits = seg_bits)
 int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,

@@ -828,7 +828,61 @@ __device__ __forceinline__ uint32_t eg_code16(uint32_t x, uint32_t& width) {
     return code;
 }
 
-template <int D>
+// Decoupled look-back (single-pass fused encode): the exclusive stream offset of segment s from the
+// look-back words of segments < s -- kLbK x 64 at a time, kLbK independent loads per lane (sc1 loads:
+// agent-scope atomics), so that a walk past the segments still in flight (thousands) takes a few
+// round trips.  A window counts once every segment up to the nearest inclusive prefix has at least its
+// aggregate; the wave re-polls otherwise.  Segments are dispatched in order and publish their aggregate
+// before they look back, so the wait is short; a bounded spin gives up (returns false) instead of hanging.
+constexpr uint64_t kLbP = 1ull << 63, kLbA = 1ull << 62, kLbVal = kLbA - 1;
+constexpr int kLbK = 1;
+__device__ __forceinline__ uint64_t lanes_upto(int fp, int k) {  // lanes l with 64k + l <= fp
+    const int r = fp - 64 * k;
+    return r < 0 ? 0ull : (r >= 63 ? ~0ull : ((2ull << r) - 1ull));
+}
+__device__ __forceinline__ bool lookback_offset(const uint64_t* st, uint64_t s, uint64_t carry, int lane,
+                                                uint64_t& excl) {
+    excl = 0;
+    int64_t j0 = (int64_t)s - 1;
+    for (uint32_t spins = 0; spins < (1u << 20);) {
+        uint64_t v[kLbK];
+#pragma unroll
+        for (int k = 0; k < kLbK; k++) {
+            const int64_t j = j0 - lane - 64 * k;
+            v[k] = j >= 0 ? __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : (kLbP | carry);  // before segment 0: the carried bits
+        }
+        int fp = 64 * kLbK;  // window index (64k + lane) of the nearest inclusive prefix
+#pragma unroll
+        for (int k = kLbK - 1; k >= 0; k--) {
+            const uint64_t pm = __ballot((v[k] & kLbP) != 0);
+            if (pm) fp = 64 * k + __builtin_ctzll(pm);
+        }
+        bool gave_up = false, missing = false;
+        uint64_t c = 0;
+#pragma unroll
+        for (int k = 0; k < kLbK; k++) {
+            const uint64_t need = lanes_upto(fp, k);
+            gave_up |= (__ballot((v[k] & (kLbP | kLbA)) == (kLbP | kLbA)) & need) != 0;
+            missing |= (__ballot((v[k] & (kLbP | kLbA)) == 0) & need) != 0;
+            c += ((need >> lane) & 1) ? (v[k] & kLbVal) : 0ull;
+        }
+        if (gave_up) return false;
+        if (missing) {  // not published yet: poll again
+            spins++;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        excl += c;
+        if (fp < 64 * kLbK) return true;
+        j0 -= 64 * kLbK;
+    }
+    return false;
+}
+
+template <int D, bool SP>
 __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, EgFusedParams E) {
     constexpr int CS = 64 * D;
     constexpr int NB = (D == 8) ? 8 : 4;
@@ -955,6 +1009,107 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     const int cp = lane >> 3, part = lane & 7;
     const bool lvalid = cube0 + cp < P.n_cubes;
     const char* cb = wl + cp * CUBE_B;
+    if constexpr (SP) {
+        // ---- single pass: lane bit counts, segment offset by look-back, words straight into place ----
+        uint32_t lb = 0;
+        if (lvalid) {
+#pragma unroll 1
+            for (int i0 = 0; i0 < VPL; i0 += 8) {
+                const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
+                const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    uint32_t width;
+                    (void)eg_code16(*(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu)), width);
+                    lb += width;
+                }
+            }
+        }
+        uint32_t incl = lb;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += t;
+        }
+        const uint32_t tot = __shfl(incl, 63, 64);
+        const uint64_t s = wid;
+        if (lane == 0) __hip_atomic_store(&E.seg_state[s], kLbA | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t base = 0;
+        const bool ok = lookback_offset(E.seg_state, s, E.carry_bits, lane, base);
+        if (lane == 0)
+            __hip_atomic_store(&E.seg_state[s], ok ? (kLbP | (base + tot)) : (kLbP | kLbA), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok) {  // the host re-runs the call with the two-pass path
+            if (lane == 0) atomicOr((unsigned int*)&E.status[1], 4u);
+            return;
+        }
+        if (lane == 0) {
+            E.seg_off[s] = base;
+            E.seg_bits[s] = tot;
+            if (cube0 + kCubesPerWave >= P.n_cubes) E.status[0] = base + tot;  // the last segment: total
+        }
+        if ((base + tot + 31) / 32 > E.out_cap_words) {  // wave-uniform; nothing is written past the end
+            if (lane == 0) atomicOr((unsigned int*)&E.status[1], 1u);
+            return;
+        }
+        // eg_compact_kernel's placement, fed word by word from the coder instead of from a slot
+        const uint64_t start = base + (incl - lb);
+        const uint32_t r = (uint32_t)(start & 31);
+        uint32_t* const outw = E.out + (start >> 5);
+        const uint32_t ndst = lb ? (uint32_t)(((start + lb - 1) >> 5) - (start >> 5) + 1) : 0u;
+        uint32_t prev = 0, first = 0, last = 0, d = 0;
+        auto put = [&](uint32_t cur) {
+            const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
+            prev = cur;
+            if (d == 0) first = v;
+            if (d == ndst - 1) last = v;
+            if (d != 0 && d != ndst - 1) outw[d] = __builtin_bswap32(v);
+            d++;
+        };
+        uint64_t acc = 0;
+        uint32_t nb = 0;
+        if (lvalid) {
+#pragma unroll 1
+            for (int i0 = 0; i0 < VPL; i0 += 8) {
+                const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
+                const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+                uint32_t v[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) v[e] = *(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    uint32_t width;
+                    const uint32_t code = eg_code16(v[e], width);
+                    acc = (acc << width) | code;
+                    nb += width;
+                    if (nb >= 32u) {
+                        nb -= 32u;
+                        put((uint32_t)(acc >> nb));
+                    }
+                }
+            }
+            if (nb) put((uint32_t)(acc << (32u - nb)));
+            if (d < ndst) put(0u);  // the last word holds only the shifted-out bits of the previous one
+        }
+        const uint32_t nlb = __shfl_down(lb, 1, 64);
+        const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
+        const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
+        const uint32_t nfirst = __shfl_down(first, 1, 64);
+        if (next_shares) last |= nfirst;
+        if (ndst == 0) return;
+        const bool shares_prev = lane > 0 && r != 0;
+        if (ndst == 1) {
+            if (lane == 0) E.head[s] = __builtin_bswap32(first);
+            else if (last_lane) E.tail[s] = __builtin_bswap32(last);
+            else outw[0] = __builtin_bswap32(last);
+            return;
+        }
+        if (lane == 0) E.head[s] = __builtin_bswap32(first);
+        else if (!shares_prev) outw[0] = __builtin_bswap32(first);
+        if (last_lane) E.tail[s] = __builtin_bswap32(last);
+        else outw[ndst - 1] = __builtin_bswap32(last);
+        return;
+    }
     // the segment's slot base is wave-uniform (scalar); each store adds a 32-bit lane offset
     char* const seg = (char*)(E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap);
     uint32_t dofs = (uint32_t)lane * 4u;  // byte offset of the lane's next word: (nw * 64 + lane) * 4
@@ -1760,10 +1915,11 @@ void launch_enc_t(const EncodeParams& P, hipStream_t st) {
     hipLaunchKernelGGL((encode_kernel<D, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
 }
 template <int D>
-void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
+void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, bool sp, hipStream_t st) {
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+    if (sp) hipLaunchKernelGGL((encode_eg_kernel<D, true>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+    else hipLaunchKernelGGL((encode_eg_kernel<D, false>), dim3(blocks), dim3(kBlock), 0, st, P, E);
 }
 template <bool NT>
 void launch_enc16(const EncodeParams& P, hipStream_t st) {
@@ -1809,10 +1965,10 @@ int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
+int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, bool single_pass, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
-    if (D == 8) launch_enc_eg_t<8>(P, E, st);
-    else launch_enc_eg_t<4>(P, E, st);
+    if (D == 8) launch_enc_eg_t<8>(P, E, single_pass, st);
+    else launch_enc_eg_t<4>(P, E, single_pass, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

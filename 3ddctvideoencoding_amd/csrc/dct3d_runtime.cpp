@@ -72,7 +72,7 @@ struct dct3d_ctx {
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
     // fused encode + Exp-Golomb: per-segment slots and lane bit counts
-    DevBuf d_egf_slot, d_egf_lbits;
+    DevBuf d_egf_slot, d_egf_lbits, d_egf_state;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
@@ -222,7 +222,8 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
                       &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
-                      &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster})
+                      &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egf_slot,
+                      &c->d_egf_lbits, &c->d_egf_state})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -780,8 +781,14 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     const uint64_t n_seg = (n_cubes + 7) / 8, n_chunks = (n_seg + 4095) / 4096;
     // worst case per lane: cs/8 values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 14 bits)
     const uint32_t seg_cap = (uint32_t)(64 * (((c->plan.cs / 8) * 27 + 31) / 32));
-    if ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
-        (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
+    // two passes (the default): K1 codes into per-segment slots, then scan + compaction.  The single pass
+    // (DCT3D_EG_SINGLE_PASS=1: K1 places the stream itself after a decoupled look-back) writes the same
+    // stream but measured slower; a look-back that gives up falls back to two passes
+    const char* one = getenv("DCT3D_EG_SINGLE_PASS");
+    bool sp = one && *one && strcmp(one, "0");
+    if ((rc = sp ? c->d_egf_state.grow(n_seg * sizeof(uint64_t)) : 0) ||
+        (rc = sp ? 0 : c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
+        (rc = sp ? 0 : c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
         (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
         (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
         return rc;
@@ -812,10 +819,14 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     E.seg_cap = seg_cap;
     E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
     E.seg_bits = (uint32_t*)c->d_eg_bits.p;
-    hipEvent_t* ev = timing_slot(c);
-    if (ev) (void)hipEventRecord(ev[0], c->stream);
-    if (launch_encode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    E.seg_state = (uint64_t*)c->d_egf_state.p;
+    E.seg_off = (uint64_t*)c->d_eg_off.p;
+    E.head = (uint32_t*)c->d_eg_ht.p;
+    E.tail = (uint32_t*)c->d_eg_ht.p + n_seg;
+    E.out = (uint32_t*)d_out;
+    E.out_cap_words = out_cap / 4;
+    E.status = (uint64_t*)c->d_eg_status.p;
+    E.carry_bits = (uint32_t)carry_bits;
     EgParams G;
     G.q = nullptr;
     G.n_cubes = n_seg;  // segments
@@ -830,13 +841,33 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     G.out_cap_words = out_cap / 4;
     G.carry_bits = (uint32_t)carry_bits;
     G.carry_byte = carry_byte;
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
     uint64_t st[2] = {0, 0};
-    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return DCT3D_EDEVICE;
+    for (;;) {
+        if (!sp && ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
+                    (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t)))))
+            return rc;
+        E.slot = (uint32_t*)c->d_egf_slot.p;
+        E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
+        if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess ||
+            (sp && hipMemsetAsync(c->d_egf_state.p, 0, n_seg * sizeof(uint64_t), c->stream) != hipSuccess))
+            return DCT3D_EDEVICE;
+        hipEvent_t* ev = timing_slot(c);
+        if (ev) (void)hipEventRecord(ev[0], c->stream);
+        if (launch_encode_eg(D, P, E, sp, c->stream)) return DCT3D_EKERNEL;
+        if (ev) (void)hipEventRecord(ev[1], c->stream);
+        if (ev) (void)hipEventRecord(ev[2], c->stream);
+        if (sp ? launch_eg_stitch(G, c->stream) : launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream))
+            return DCT3D_EKERNEL;
+        if (ev) (void)hipEventRecord(ev[3], c->stream);
+        if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return DCT3D_EDEVICE;
+        if (sp && (st[1] & 4)) {  // a look-back gave up (never expected): the two-pass path
+            sp = false;
+            continue;
+        }
+        break;
+    }
     if (total_bits) *total_bits = st[0];
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     if (st[1] & 1) return DCT3D_ENOSPC;

@@ -90,7 +90,26 @@ def test_fused_1080p_matches_oracle(pkg, oracle, plan8, gpu_ctx8):
     assert tb == ebits and got == exp
 
 
-def test_fused_capacity(pkg, gpu_ctx8):
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["uniform", "checker"])
+@pytest.mark.parametrize("carry_bits", [0, 5])
+def test_fused_single_pass_matches_two_pass(pkg, gpu_ctx8, gpu_ctx4, monkeypatch, depth, kind, carry_bits):
+    """DCT3D_EG_SINGLE_PASS=1 (each wave places its bits after a decoupled look-back over the earlier
+    segments' totals) and the default two passes (slots + scan + compaction) write the same stream;
+    1080p x 3 stacks is ~49k segments, so look-backs run across many waves still in flight"""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = _content(pkg, kind, 1920, 1080, 3 * depth) if kind != "uniform" else \
+        pkg.synthetic.frames(1920, 1080, 3 * depth, kind="uniform", frame0=11)
+    tp, ttp, _ = _fused(ctx, fr, 0xA5, carry_bits)
+    monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
+    sp, tsp, _ = _fused(ctx, fr, 0xA5, carry_bits)
+    assert tsp == ttp and sp == tp
+
+
+@pytest.mark.parametrize("single_pass", [False, True])
+def test_fused_capacity(pkg, gpu_ctx8, monkeypatch, single_pass):
+    if single_pass:
+        monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
     fr = pkg.synthetic.frames(64, 64, 8, kind="uniform")
     _, tb, _ = _fused(gpu_ctx8, fr)
     import torch
@@ -100,7 +119,9 @@ def test_fused_capacity(pkg, gpu_ctx8):
     with pytest.raises(pkg.Dct3dError) as ei:
         gpu_ctx8.encode_eg_dev(d, 64, 64, 1, out, small)
     assert ei.value.code == pkg.DCT3D_ENOSPC
-    assert (out.cpu().numpy() == 7).all()          # nothing written
+    o = out.cpu().numpy()
+    assert (o[small // 4:] == 7).all()             # nothing written past out_cap
+    assert single_pass or (o == 7).all()           # two passes: nothing written at all
     got, tb2, _ = _fused(gpu_ctx8, fr, cap=(tb + 31) // 32 * 4)   # exactly enough
     assert tb2 == tb
 
