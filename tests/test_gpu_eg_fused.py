@@ -62,6 +62,22 @@ def test_fused_ragged_segment_tails(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx
     assert tb == ebits and got == exp
 
 
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("w,h,stacks", [(8, 8, 1), (40, 8, 5), (136, 72, 2)])
+@pytest.mark.parametrize("carry_bits", [0, 3])
+def test_fused_single_pass_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, monkeypatch, depth, w, h,
+                                          stacks, carry_bits):
+    """DCT3D_EG_SINGLE_PASS=1 on small and ragged inputs (one segment, a partial last segment, the
+    carried byte taken by segment 0's look-back) against the oracle's stream"""
+    monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    fr = pkg.synthetic.frames(w, h, stacks * depth, kind="uniform", frame0=w + carry_bits)
+    exp, ebits = _expected(oracle, pkg, plan.encode_q(fr), depth, 0x3C, carry_bits)
+    got, tb, raw = _fused(ctx, fr, 0x3C, carry_bits)
+    assert tb == ebits and got == exp
+    assert not raw[len(got):(tb + 31) // 32 * 4].any()
+
+
 @pytest.mark.parametrize("carry_bits", range(8))
 def test_fused_carry_partial_byte(pkg, oracle, plan8, gpu_ctx8, carry_bits):
     fr = pkg.synthetic.frames(48, 40, 8, kind="uniform", frame0=carry_bits)
