@@ -533,6 +533,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
             atomicOr((unsigned int*)&P.status[2], 2u);
             return;
         }
+        // one step = a run of 1-bit codes, then one longer code (as sync_step): every lane advances
+        // through both halves each iteration, instead of the wave running a run-only and a code-only
+        // iteration for lanes that are in different halves
         const uint32_t room = min(min(end - p0, limit - p0), rem - i);
         const uint32_t k = r.ones(min(room, 64u));
         if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
@@ -540,15 +543,16 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
                 mk[(ph + j) / kMarkVals] = base + p0 + (j - i);
             i += k;
             if (ends_here && i == rem) P.status[1] = base + r.pos;  // the bit after the last wanted value
-            continue;
         }
-        if (!r.at_long_code()) continue;  // refill
+        // the run ended the chunk or the wanted values, or the buffered bits ran out inside it (refill)
+        if (i >= rem || r.pos >= end || !r.at_long_code()) continue;
+        const uint32_t p1 = r.pos;
         if (!r.get(code) || r.pos > limit) {
             // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
-            atomicOr((unsigned int*)&P.status[2], (uint64_t)p0 + 32 <= limit && r.pos <= limit ? 1u : 2u);
+            atomicOr((unsigned int*)&P.status[2], (uint64_t)p1 + 32 <= limit && r.pos <= limit ? 1u : 2u);
             return;
         }
-        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p0;
+        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p1;
         if (++i == rem && ends_here) P.status[1] = base + r.pos;
     }
 }
