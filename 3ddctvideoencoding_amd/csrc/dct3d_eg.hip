@@ -442,7 +442,17 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     bool invalid = false;
     if (live) {
         r.seek(s0);
-        // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary
+        // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary.
+        // The chunk interior first, without bounds (a step moves at most 64 + 63 bits; as the mark
+        // pass), then the checked steps; an invalid code leaves the lean loop unconsumed.
+        const uint32_t fast_stop = stop > 128u ? stop - 128u : 0u;
+        while (r.pos < fast_stop) {
+            n += r.ones(64u);
+            if (!r.at_long_code()) continue;  // refill
+            uint32_t code;
+            if (!r.get(code)) break;
+            n++;
+        }
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
         }
     }
@@ -527,6 +537,25 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
     uint64_t* const mk = P.mark + (idx0 / kMarkVals);  // mark[(idx0 + i) / 32] = mk[(ph + i) / 32]
     uint32_t i = 0, code;
+    // Interior of the chunk: a step moves at most 64 + 63 bits and 65 values, so while the parse is
+    // 128 bits short of the chunk end and of the data limit, and 66 values short of the wanted count,
+    // none of the bounds below can bind -- a lean loop without them (a 32-zero-bit invalid code leaves
+    // it for the checked loop, which reports it).
+    const uint32_t lim_end = min(end, limit);
+    const uint32_t fast_end = lim_end > 128u ? lim_end - 128u : 0u;
+    const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
+    while (r.pos < fast_end && i < fast_rem) {
+        const uint32_t p0 = r.pos;
+        const uint32_t k = r.ones(64u);
+        for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
+            mk[(ph + j) / kMarkVals] = base + p0 + (j - i);
+        i += k;
+        if (!r.at_long_code()) continue;  // refill
+        const uint32_t p1 = r.pos;
+        if (!r.get(code)) break;  // invalid: nothing consumed, the checked loop reports it
+        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p1;
+        i++;
+    }
     while (i < rem && r.pos < end) {
         const uint32_t p0 = r.pos;
         if (p0 >= limit) {  // ran out of bits

@@ -107,7 +107,8 @@ struct WinReader {
     uint64_t buf;    // left-aligned bits [pos, pos + avail)
     int avail;
     uint32_t pos;
-    uint32_t pre;
+    uint32_t pre;    // word `next` as read: zeroed past the window only where it is used, so that the
+                     // LDS read's wait falls at the next refill, not right behind the read
     __device__ __forceinline__ uint32_t word(uint32_t i) const {
         const uint32_t v = s[i < n ? i : 0u];  // unconditional read
         return i < n ? v : 0u;
@@ -119,13 +120,14 @@ struct WinReader {
         buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
         avail = 64 - sh;
         next = k + 2;
-        pre = word(next);
+        pre = s[next < n ? next : 0u];
     }
     __device__ __forceinline__ void refill() {
         if (avail <= 32) {
-            buf |= (uint64_t)pre << (32 - avail);
+            buf |= (uint64_t)(next < n ? pre : 0u) << (32 - avail);
             avail += 32;
-            pre = word(++next);
+            ++next;
+            pre = s[next < n ? next : 0u];
         }
     }
     __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
