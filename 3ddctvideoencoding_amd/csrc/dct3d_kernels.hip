@@ -1647,7 +1647,21 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_values)
     const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* win = (uint32_t*)wl;
-    for (uint32_t i = lane; i < nwin; i += 64) win[i] = stream_word(E, w0 + i);
+    // 4 words per lane per round, all loads issued before the first LDS write: a one-word loop waited
+    // out a full global round trip per 64 words (3 for ramp content, 6+ for noise)
+    for (uint32_t i0 = 0; i0 < nwin; i0 += 256) {
+        uint32_t t[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t i = i0 + b * 64 + lane;
+            t[b] = E.words[min(w0 + i, E.n_words - 1)];  // unconditional (a load under a branch is waited at the join)
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t i = i0 + b * 64 + lane;
+            if (i < nwin) win[i] = w0 + i < E.n_words ? __builtin_bswap32(t[b]) : 0u;
+        }
+    }
     wave_lds_sync();
     int32_t v[32];
     parse_values<32>(E, win, nwin, w0, fits, my, v);
