@@ -608,7 +608,18 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const bool fits = span <= kEmitWinWords;  // wave-uniform
     const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* wl = lds[wave];
-    for (uint32_t i = lane; i < nwin; i += 64) wl[i] = stream_word(P, w0 + i);
+    // 4 loads in flight per lane before the LDS writes (as decode_eg_kernel's staging)
+    const uint32_t nst = P.n_words ? nwin : 0u;  // (an empty stream: reported by the mark pass)
+    for (uint32_t i0 = 0; i0 < nst; i0 += 256) {
+        uint32_t t[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) t[b] = P.words[min(w0 + i0 + b * 64 + lane, P.n_words - 1)];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const uint32_t i = i0 + b * 64 + lane;
+            if (i < nwin) wl[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
+        }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -1649,7 +1649,10 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     uint32_t* win = (uint32_t*)wl;
     // 4 words per lane per round, all loads issued before the first LDS write: a one-word loop waited
     // out a full global round trip per 64 words (3 for ramp content, 6+ for noise)
-    for (uint32_t i0 = 0; i0 < nwin; i0 += 256) {
+    // (an empty stream never gets here: the mark pass reported it, status[2]; the guard keeps the
+    // clamped index below in range regardless, outside the loop so the loads stay unconditional)
+    const uint32_t nst = E.n_words ? nwin : 0u;
+    for (uint32_t i0 = 0; i0 < nst; i0 += 256) {
         uint32_t t[4];
 #pragma unroll
         for (int b = 0; b < 4; b++) {
