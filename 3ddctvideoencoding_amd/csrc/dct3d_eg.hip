@@ -375,7 +375,21 @@ __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t
 // the block's window: chunks [first, first + kEgBlock) plus slack, coalesced, then a barrier
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win, uint64_t first) {
     const uint64_t w0 = (P.start_bit + first * kChunkBits) >> 5;
-    for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += kEgBlock) win[i] = stream_word(P, w0 + i);
+    // all of a thread's loads in flight at once (clamped, unconditional): the one-word loop under a
+    // bounds branch waited out a full global round trip per 256 words, 17 per block
+    constexpr uint32_t kR = (kSyncWinWords + kEgBlock - 1) / kEgBlock;
+    if (P.n_words) {  // block-uniform
+        uint32_t t[kR];
+#pragma unroll
+        for (uint32_t b = 0; b < kR; b++) t[b] = P.words[min(w0 + threadIdx.x + b * kEgBlock, P.n_words - 1)];
+#pragma unroll
+        for (uint32_t b = 0; b < kR; b++) {
+            const uint32_t i = threadIdx.x + b * kEgBlock;
+            if (i < kSyncWinWords) win[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += kEgBlock) win[i] = 0u;
+    }
     __syncthreads();
     return LdsBits{win, w0, kSyncWinWords};
 }
