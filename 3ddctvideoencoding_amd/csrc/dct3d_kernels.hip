@@ -904,7 +904,14 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     const uint32_t cube0 = wid * kCubesPerWave;
     uint2 raw[D];
     load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
-    for (int i = threadIdx.x; i < CS; i += kBlock) s_pos[i] = (uint16_t)(2 * E.diag[i]);
+    {  // both loads in flight before the LDS writes (a strided loop waited one round trip per pass)
+        static_assert(CS % kBlock == 0, "whole passes");
+        uint16_t t[CS / kBlock];
+#pragma unroll
+        for (int r = 0; r < CS / kBlock; r++) t[r] = E.diag[threadIdx.x + r * kBlock];
+#pragma unroll
+        for (int r = 0; r < CS / kBlock; r++) s_pos[threadIdx.x + r * kBlock] = (uint16_t)(2 * t[r]);
+    }
     __syncthreads();
     if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
     enc_tables(P, s_tab, lane);
@@ -1629,7 +1636,14 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];
     if (E.status[2] != 0) return;  // corrupt / short stream: reported by the mark pass (block-uniform)
-    for (uint32_t i = threadIdx.x; i < CS; i += kBlock) s_diag[i] = E.diag[i];
+    {  // both loads in flight before the LDS writes
+        static_assert(CS % kBlock == 0, "whole passes");
+        uint16_t t[CS / kBlock];
+#pragma unroll
+        for (uint32_t r = 0; r < CS / kBlock; r++) t[r] = E.diag[threadIdx.x + r * kBlock];
+#pragma unroll
+        for (uint32_t r = 0; r < CS / kBlock; r++) s_diag[threadIdx.x + r * kBlock] = t[r];
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
