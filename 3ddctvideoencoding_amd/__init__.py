@@ -171,7 +171,7 @@ def eg_stream_bytes(total_bits: int) -> int:
 
 class Context:
     """dct3d_ctx: one per device (the MI355X equivalent of the reference's per-call OpenCL setup,
-    encoder.c:169-219).  Block dims are codec.h's DCT_BLOCK_WIDTH/HEIGHT/DEPTH (8x8x8 or 8x8x4)."""
+    encoder.c:147-197).  Block dims are codec.h's DCT_BLOCK_WIDTH/HEIGHT/DEPTH (8x8x8 or 8x8x4)."""
 
     def __init__(self, device: int = 0, block_w: int = 8, block_h: int = 8, block_d: int = 8):
         h = C.c_void_p()

@@ -31,10 +31,17 @@ struct EncodeParams {
     const float* tab_rstep;    // [32] fp32(1/step_s)
     const float* tab_G;        // [32]
     const float* tab_E;        // [32]
+    // 8x8x4 (encode_kernel): uncertified coefficients go to a flag list for encode_fixup_kernel
     unsigned long long* flag_list;
     unsigned int* counters;    // [0] flagged coefficients, [1] overflow cubes
     uint32_t flag_cap;
     uint32_t* cube_list;       // capacity n_cubes
+    // 8x8x8 (encode16_kernel): uncertified coefficients replayed inside the wave (exact Java fold)
+    const int32_t* ngroups;    // [cs] exact replay tables (as FixupParams)
+    const double* coef;        // [cs * kMaxGroupsDev]
+    const uint8_t* group_of;   // [cs * cs]
+    unsigned int* replay_count;  // this call's counter slot (coefficients replayed), or nullptr
+    unsigned int* replay_clear;  // the other slot: zeroed by the launch for the next call, or nullptr
 };
 
 struct FixupParams {
@@ -92,6 +99,9 @@ struct Fwd64Params {
 int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st);
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
 int launch_encode(int D, const EncodeParams& P, hipStream_t st);
+// true when launch_encode(D) replays uncertified coefficients itself (encode16_kernel: 8x8x8), i.e. the
+// call needs no counter reset and no encode_fixup_kernel
+bool encode_replays_inwave(int D);
 int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st);  // diagnostic
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
 struct EgParams {

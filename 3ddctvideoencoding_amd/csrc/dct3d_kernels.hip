@@ -454,6 +454,98 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), s_tab, lane, cube0);
 }
 
+// =============================================================================================
+// Exact Java fold for flagged (cube, k): out = JavaRound(fold_g(S_g * coef_g) / step)
+// =============================================================================================
+// The Java fold of DCT.java:44-52 for coefficient k of cube g, by one whole wave:
+//   out = sum over groups gi (HashMap order) of  S_gi * coef_gi,  S_gi = exact integer pixel sums.
+// Group sums: LDS integer atomics (exact).  Products: one lane per group, in parallel (each is one
+// correctly rounded fp64 multiply, as in Java).  The fold itself (the only order-dependent part) runs
+// on lane 0 over the products in LDS.  ssum / prod: the wave's kMaxGroupsDev-entry scratch.  The
+// result is valid in lane 0.
+struct ReplayGeom {
+    const uint8_t* raster;
+    uint32_t cubes_per_stack, nbx, width;
+    uint64_t plane, stack_stride;
+    const int32_t* ngroups;
+    const double* coef;
+    const uint8_t* group_of;
+};
+// The global loads of one replay (split from the fold so that a caller can issue them early: on gfx9
+// a load issued after a wave's stores waits for those stores too, vmcnt being one in-order counter).
+struct ReplayIn {
+    int ng;
+    double cf;
+    uint2 px, gr;
+};
+template <int D>
+__device__ __forceinline__ ReplayIn replay_load(const ReplayGeom& R, uint32_t g, uint32_t k, int lane) {
+    constexpr int CS = 64 * D;
+    ReplayIn in;
+    in.ng = R.ngroups[k];
+    in.cf = R.coef[(size_t)k * kMaxGroupsDev + lane];  // lanes >= ng: unused
+    in.px = in.gr = make_uint2(0u, 0u);
+    if (lane * 8 < CS) {
+        const int z = lane >> 3, y = lane & 7;
+        const uint32_t s = g / R.cubes_per_stack;
+        const uint32_t r = g - s * R.cubes_per_stack;
+        const uint32_t by = r / R.nbx, bx = r - by * R.nbx;
+        const uint8_t* src = R.raster + (size_t)s * R.stack_stride + (size_t)z * R.plane +
+                             (size_t)(by * 8 + y) * R.width + bx * 8;
+        in.px = *(const uint2*)src;
+        in.gr = *(const uint2*)(R.group_of + (size_t)k * CS + lane * 8);
+    }
+    return in;
+}
+// LEAN: the fold loop is not unrolled (in-wave replay: its registers would count against the main path)
+template <int D, bool LEAN = false>
+__device__ __forceinline__ int replay_fold(const ReplayIn& in, uint32_t k, int lane, int* ssum, double* prod) {
+    constexpr int CS = 64 * D;
+    ssum[lane] = 0;
+    wave_lds_sync();
+    if (lane * 8 < CS) {
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) {
+            const uint32_t g0 = (in.gr.x >> (8 * bb)) & 0xFF, g1 = (in.gr.y >> (8 * bb)) & 0xFF;
+            if (g0 < kMaxGroupsDev) atomicAdd(&ssum[g0], (int)((in.px.x >> (8 * bb)) & 0xFF));
+            if (g1 < kMaxGroupsDev) atomicAdd(&ssum[g1], (int)((in.px.y >> (8 * bb)) & 0xFF));
+        }
+    }
+    wave_lds_sync();
+    prod[lane] = __dmul_rn((double)ssum[lane], lane < in.ng ? in.cf : 0.0);
+    wave_lds_sync();
+    int q = 0;
+    if (lane == 0) {
+        const int ng = in.ng;
+        double acc = 0.0;
+        int gi = 0;
+        if constexpr (LEAN) {
+#pragma unroll 1
+            for (; gi + 4 <= ng; gi += 4) {  // DCT.java:50, output += sum * coefficient, in order
+                const double p0 = prod[gi], p1 = prod[gi + 1], p2 = prod[gi + 2], p3 = prod[gi + 3];
+                acc = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(acc, p0), p1), p2), p3);
+            }
+        } else {
+            for (; gi + 4 <= ng; gi += 4) {
+                const double p0 = prod[gi], p1 = prod[gi + 1], p2 = prod[gi + 2], p3 = prod[gi + 3];
+                acc = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(acc, p0), p1), p2), p3);
+            }
+        }
+#pragma unroll 1
+        for (; gi < ng; gi++) acc = __dadd_rn(acc, prod[gi]);
+        const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+        const int st = max(1, 5 * (kx + ky + kz));
+        q = java_round_dev(__ddiv_rn(acc, (double)st));
+    }
+    wave_lds_sync();
+    return q;
+}
+template <int D>
+__device__ __forceinline__ int exact_coef(const ReplayGeom& R, uint32_t g, uint32_t k, int lane, int* ssum,
+                                          double* prod) {
+    return replay_fold<D>(replay_load<D>(R, g, k, lane), k, lane, ssum, prod);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Encode, 16 lanes per cube (8x8x8): the decode's geometry in the forward direction.  Lane (c, k, h)
 // of the wave's 4 cubes: c = (lane >> 5) * 2 + ((lane & 15) >> 3), k = lane & 7, h = (lane >> 4) & 1
@@ -489,10 +581,10 @@ __device__ __forceinline__ void e16_load(const EncodeParams& P, uint32_t g, bool
     }
 }
 
-// Statistics, passes X / Z / Y, quantise + certify, exact DC.  Uncertified coefficients are appended
-// to the flag list; overflow = 1: the list is full, the cube goes to the whole-cube replay.
+// Statistics, passes X / Z / Y, quantise + certify, exact DC.  Uncertified coefficients are returned
+// as the lane's mask fm (bit 4 ky + e: coefficient (kz = k, ky, kx = 4h + e)); the caller replays them.
 __device__ __forceinline__ void e16_body(const EncodeParams& P, const uint2 (&raw)[4], char* wl, const float4* tab,
-                                         int lane, uint32_t g, bool valid, int32_t (&qv)[8][4], int& overflow) {
+                                         int lane, bool valid, int32_t (&qv)[8][4], uint32_t& fm) {
     constexpr int CS = 512;
     const int k = lane & 7, h = (lane >> 4) & 1;
     const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
@@ -601,41 +693,45 @@ __device__ __forceinline__ void e16_body(const EncodeParams& P, const uint2 (&ra
         for (int y = 0; y < 8; y++) b[y][e] = col[y];
     }
 
-    // ---- quantise + certify; uncertified coefficients appended while q is in registers ----
+    // ---- quantise + certify; uncertified coefficients recorded in fm while q is in registers ----
     int sz = k + 4 * h;
     float rr[11], thr[11];
-    overflow = 0;
+    fm = 0u;
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         pin(b[ky]);
         tab_window<4, 11>(tab, sz, ky, A, rr, thr);
-        bool f = false;
-        float qq[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            qq[e] = b[ky][e] * rr[ky + e];
-            const float n = __builtin_rintf(qq[e]);
-            f |= __builtin_fabsf(qq[e] - n) >= thr[ky + e];
+            const float qq = b[ky][e] * rr[ky + e];
+            const float n = __builtin_rintf(qq);
+            fm |= (__builtin_fabsf(qq - n) >= thr[ky + e] ? 1u : 0u) << (4 * ky + e);
             qv[ky][e] = (int32_t)n;
         }
-        if (__builtin_expect(f && valid, 0)) {
-#pragma unroll
-            for (int e = 0; e < 4; e++)
-                if (__builtin_fabsf(qq[e] - __builtin_rintf(qq[e])) >= thr[ky + e]) {
-                    const uint32_t kk = (uint32_t)((k * 8 + ky) * 8 + 4 * h + e);
-                    const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                    if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + kk;
-                    else overflow = 1;
-                }
-        }
         pin(qv[ky]);
-        asm volatile("" : "+v"(overflow));
+        asm volatile("" : "+v"(fm));
     }
-    if (k == 0 && h == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC
+    if (k == 0 && h == 0) {
+        qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (the single Java group)
+        fm &= ~1u;
+    }
+    if (!valid) fm = 0u;
+}
+
+// In-wave exact replay (encode16): the uncertified coefficient at bit `bit` of lane src's mask fm
+// (bit 4 ky + e of lane (c, k, h): coefficient (kz = k, ky, kx = 4h + e) of cube cube0 + c).
+__device__ __forceinline__ void e16_flag_pos(uint32_t fm, int src, uint32_t cube0, uint32_t& g, uint32_t& kk) {
+    const int bit = __shfl(fm ? __builtin_ctz(fm) : 0, src, 64);
+    const int sk = src & 7, sh = (src >> 4) & 1, sc = (src >> 5) * 2 + ((src & 15) >> 3);
+    g = cube0 + sc;
+    kk = (uint32_t)((sk * 8 + (bit >> 2)) * 8 + 4 * sh + (bit & 3));
 }
 
 // MEM (dct3d_encode_memonly_dev, DIAGNOSTIC: the output is NOT a DCT): the same loads, staging and
-// stores with the transform, quantisation and certification replaced by a few integer ops
+// stores with the transform, quantisation and certification replaced by a few integer ops.
+// One launch is the whole encode: no flag list, no counter reset, no fixup launch.  Block 0 zeroes the
+// next call's replay counter slot (P.replay_clear; the two slots alternate between calls).
+static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the wave's region");
 template <bool NT, bool MEM = false>
 __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
@@ -649,10 +745,11 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     const bool valid = g < P.n_cubes;
     uint2 raw[4];
     e16_load(P, g, valid, k, h, raw);
+    if (!MEM && blockIdx.x == 0 && threadIdx.x == 0 && P.replay_clear) *P.replay_clear = 0u;
     if (cube0 >= P.n_cubes) return;  // wave-uniform
     char* wl = lds + wave * kE16Lds;
     int32_t qv[8][4];
-    int overflow = 0;
+    uint32_t fm = 0u;
     if constexpr (MEM) {
 #pragma unroll
         for (int ky = 0; ky < 8; ky++)
@@ -660,7 +757,19 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
             for (int e = 0; e < 4; e++) qv[ky][e] = (int32_t)(((ky & 1) ? raw[e].y : raw[e].x) >> (ky * 3 % 24)) & 255;
     } else {
         enc_tables(P, s_tab, lane);
-        e16_body(P, raw, wl, s_tab, lane, g, valid, qv, overflow);
+        e16_body(P, raw, wl, s_tab, lane, valid, qv, fm);
+    }
+
+    // ---- rare path, part 1: the first uncertified coefficient's replay loads, issued before the
+    //      stores (a load issued after them would wait for them: one in-order vmcnt) ----
+    const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
+                       P.ngroups, P.coef, P.group_of};
+    const bool rare = !MEM && __ballot(fm != 0u) != 0ull;  // wave-uniform
+    ReplayIn rin;
+    uint32_t rg = 0, rk = 0;
+    if (__builtin_expect(rare, 0)) {
+        e16_flag_pos(fm, (int)__builtin_ctzll(__ballot(fm != 0u)), cube0, rg, rk);
+        rin = replay_load<8>(R, rg, rk, lane);
     }
 
     // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
@@ -686,15 +795,28 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
         }
         wave_lds_sync();
     }
-    // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
-    const unsigned long long ov = __ballot(overflow != 0);
-    if (__builtin_expect(ov != 0ull, 0)) {
-        const int base = (lane & 32) + (lane & 8);
-        const unsigned long long cmask = (0xFFull << base) | (0xFFull << (base + 16));
-        if (overflow && (int)__builtin_ctzll(ov & cmask) == lane) {
-            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
+
+    // ---- rare path, part 2: the exact Java fold of every uncertified coefficient (whole wave, one at
+    //      a time), written over the stored value by lane 0.  The wave's own earlier store of that word
+    //      is complete first (vmcnt(0)), so the exact value is the one that stays. ----
+    if (__builtin_expect(rare, 0)) {
+        char* rs = wl;  // the wave's region is free again (its last staging round is stored)
+        uint32_t n = 0;
+        for (;;) {
+            const int q = replay_fold<8, true>(rin, rk, lane, (int*)rs, (double*)(rs + kMaxGroupsDev * 4));
+            if (lane == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                P.out[(size_t)rg * CS + rk] = q;
+            }
+            n++;
+            const int src = (int)__builtin_ctzll(__ballot(fm != 0u));  // the coefficient just replayed
+            if (lane == src) fm &= fm - 1u;
+            const uint64_t who = __ballot(fm != 0u);
+            if (who == 0ull) break;
+            e16_flag_pos(fm, (int)__builtin_ctzll(who), cube0, rg, rk);
+            rin = replay_load<8>(R, rg, rk, lane);
         }
+        if (lane == 0 && P.replay_count) atomicAdd(P.replay_count, n);
     }
 }
 
@@ -717,67 +839,6 @@ __global__ __launch_bounds__(kBlock, 4) void encode_memonly_kernel(EncodeParams 
 #pragma unroll
         for (int x = 0; x < NB; x++) qv[ky][x] = (int32_t)((ky & 1 ? raw[x % D].y : raw[x % D].x) >> (ky * 3 % 24)) & 255;
     enc_stage_store<D, true>(P, qv, lds + wave * enc_wave_lds<D>(), lane, cube0);
-}
-
-// =============================================================================================
-// Exact Java fold for flagged (cube, k): out = JavaRound(fold_g(S_g * coef_g) / step)
-// =============================================================================================
-// The Java fold of DCT.java:44-52 for coefficient k of cube g, by one whole wave:
-//   out = sum over groups gi (HashMap order) of  S_gi * coef_gi,  S_gi = exact integer pixel sums.
-// Group sums: LDS integer atomics (exact).  Products: one lane per group, in parallel (each is one
-// correctly rounded fp64 multiply, as in Java).  The fold itself (the only order-dependent part) runs
-// on lane 0 over the products in LDS.  ssum / prod: the wave's kMaxGroupsDev-entry scratch.  The
-// result is valid in lane 0.
-struct ReplayGeom {
-    const uint8_t* raster;
-    uint32_t cubes_per_stack, nbx, width;
-    uint64_t plane, stack_stride;
-    const int32_t* ngroups;
-    const double* coef;
-    const uint8_t* group_of;
-};
-template <int D>
-__device__ __forceinline__ int exact_coef(const ReplayGeom& R, uint32_t g, uint32_t k, int lane, int* ssum,
-                                          double* prod) {
-    constexpr int CS = 64 * D;
-    const int ng = R.ngroups[k];
-    const double cf = lane < ng ? R.coef[(size_t)k * kMaxGroupsDev + lane] : 0.0;  // issued early
-    ssum[lane] = 0;
-    wave_lds_sync();
-    if (lane * 8 < CS) {
-        const int z = lane >> 3, y = lane & 7;
-        const uint32_t s = g / R.cubes_per_stack;
-        const uint32_t r = g - s * R.cubes_per_stack;
-        const uint32_t by = r / R.nbx, bx = r - by * R.nbx;
-        const uint8_t* src = R.raster + (size_t)s * R.stack_stride + (size_t)z * R.plane +
-                             (size_t)(by * 8 + y) * R.width + bx * 8;
-        const uint2 px = *(const uint2*)src;
-        const uint2 gr = *(const uint2*)(R.group_of + (size_t)k * CS + lane * 8);
-#pragma unroll
-        for (int bb = 0; bb < 4; bb++) {
-            const uint32_t g0 = (gr.x >> (8 * bb)) & 0xFF, g1 = (gr.y >> (8 * bb)) & 0xFF;
-            if (g0 < kMaxGroupsDev) atomicAdd(&ssum[g0], (int)((px.x >> (8 * bb)) & 0xFF));
-            if (g1 < kMaxGroupsDev) atomicAdd(&ssum[g1], (int)((px.y >> (8 * bb)) & 0xFF));
-        }
-    }
-    wave_lds_sync();
-    prod[lane] = __dmul_rn((double)ssum[lane], cf);
-    wave_lds_sync();
-    int q = 0;
-    if (lane == 0) {
-        double acc = 0.0;
-        int gi = 0;
-        for (; gi + 4 <= ng; gi += 4) {  // DCT.java:50, output += sum * coefficient, in order
-            const double p0 = prod[gi], p1 = prod[gi + 1], p2 = prod[gi + 2], p3 = prod[gi + 3];
-            acc = __dadd_rn(__dadd_rn(__dadd_rn(__dadd_rn(acc, p0), p1), p2), p3);
-        }
-        for (; gi < ng; gi++) acc = __dadd_rn(acc, prod[gi]);
-        const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-        const int st = max(1, 5 * (kx + ky + kz));
-        q = java_round_dev(__ddiv_rn(acc, (double)st));
-    }
-    wave_lds_sync();
-    return q;
 }
 
 // One wave per uncertified coefficient (flag list), then every coefficient of the whole-cube list.
@@ -810,7 +871,7 @@ __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
 }
 
 // =============================================================================================
-// Fused encode + Exp-Golomb, K1 (dct3d_encode_eg_dev; encoder.c:228-296 up to the deflate)
+// Fused encode + Exp-Golomb, K1 (dct3d_encode_eg_dev; encoder.c:206-274 up to the deflate)
 // =============================================================================================
 // The wave's 8 cubes: rows -> transform -> quantise + certify exactly as encode_body, but the
 // uncertified coefficients are recorded in a per-lane bit mask (bit ky*NB + x) and replayed by the
@@ -1924,27 +1985,11 @@ int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, un
 // =============================================================================================
 // Launchers
 // =============================================================================================
-// Encode variants (DCT3D_ENC_VARIANT, test/bench knob): 8 lanes per cube (encode_kernel): 0 plain
-// stores, 1 non-temporal stores of the int32 output, 2 non-temporal stores and loads; 6: 16 lanes per
-// cube (encode16_kernel, 8x8x8 only), NT stores.  Defaults: 6 for 8x8x8 (ramp content 1.986 vs 1.998 ms,
-// uniform noise 2.52 vs 2.83 ms against variant 1), 1 for 8x8x4 (profiles/r01/encode_variant_sweep.txt).
+// Encode: 8x8x8 = encode16_kernel (16 lanes per cube, in-wave exact replay, one launch per call);
+// 8x8x4 = encode_kernel<4> (8 lanes per cube, flag list + encode_fixup_kernel).  Both store the int32
+// output non-temporally.  The variants that lost (8 lanes per cube at 8x8x8, plain stores, NT loads,
+// LDS-padded occupancy) are recorded in profiles/r01/encode_variant_sweep.txt, not built.
 namespace {
-constexpr int kDefaultVariant = -1;
-// Occupancy knob (DCT3D_*_LDS_PAD_KB): extra dynamic LDS per block limits the blocks per CU.  HBM3E
-// serves the encode's 1:4 read/write stream faster from fewer concurrent waves (tools/hbm_probe.hip:
-// 5.68 TB/s at 8 waves/CU against 5.36 at 32), but both kernels need the occupancy to hide their own
-// latency (tools/occupancy_sweep.sh), so the default pad is 0.
-static size_t lds_pad(const char* var, int dflt_kb) {
-    const char* e = getenv(var);
-    return (size_t)(e ? atoi(e) : dflt_kb) * 1024;
-}
-template <int D, bool NT, bool NTL = false>
-void launch_enc_t(const EncodeParams& P, hipStream_t st) {
-    static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);
-    const uint32_t groups = (P.n_cubes - P.g_base + kCubesPerWave - 1) / kCubesPerWave;
-    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    hipLaunchKernelGGL((encode_kernel<D, NT, NTL>), dim3(blocks), dim3(kBlock), pad, st, P);
-}
 template <int D>
 void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, bool sp, hipStream_t st) {
     const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
@@ -1952,47 +1997,37 @@ void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, bool sp, hip
     if (sp) hipLaunchKernelGGL((encode_eg_kernel<D, true>), dim3(blocks), dim3(kBlock), 0, st, P, E);
     else hipLaunchKernelGGL((encode_eg_kernel<D, false>), dim3(blocks), dim3(kBlock), 0, st, P, E);
 }
-template <bool NT>
+template <bool MEM>
 void launch_enc16(const EncodeParams& P, hipStream_t st) {
     const uint32_t groups = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    static const size_t pad = lds_pad("DCT3D_ENC_LDS_PAD_KB", 0);  // occupancy knob (see lds_pad)
-    hipLaunchKernelGGL((encode16_kernel<NT>), dim3(blocks), dim3(kBlock), pad, st, P);
-}
-template <int D>
-void launch_enc_variant(int v, const EncodeParams& P, hipStream_t st) {
-    if (D == 8 && v == 6) return launch_enc16<true>(P, st);
-    switch (v) {
-        case 0: launch_enc_t<D, false>(P, st); break;
-        case 2: launch_enc_t<D, true, true>(P, st); break;
-        default: launch_enc_t<D, true>(P, st); break;
-    }
+    hipLaunchKernelGGL((encode16_kernel<true, MEM>), dim3(blocks), dim3(kBlock), 0, st, P);
 }
 }  // namespace
 
+bool encode_replays_inwave(int D) { return D == 8; }
+
 int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
-    // read per launch (a getenv is ~100 ns against a ~2 ms launch): tests switch variants in-process
-    const char* e = getenv("DCT3D_ENC_VARIANT");
-    const int variant = e ? atoi(e) : kDefaultVariant;  // -1: the depth's default
-    if (D == 8) launch_enc_variant<8>(variant < 0 ? 6 : variant, P, st);
-    else launch_enc_variant<4>(variant < 0 ? 1 : variant, P, st);
+    if (D == 8) {
+        launch_enc16<false>(P, st);
+    } else {
+        const uint32_t groups = (P.n_cubes - P.g_base + kCubesPerWave - 1) / kCubesPerWave;
+        const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+        hipLaunchKernelGGL((encode_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, st, P);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
-    const char* ev = getenv("DCT3D_ENC_VARIANT");
-    if (D == 8 && (!ev || atoi(ev) == 6 || atoi(ev) < 0)) {  // the twin of the default 16-lane kernel
-        const uint32_t groups16 = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
-        hipLaunchKernelGGL((encode16_kernel<true, true>), dim3((groups16 + kWavesPerBlock - 1) / kWavesPerBlock),
-                           dim3(kBlock), lds_pad("DCT3D_ENC_LDS_PAD_KB", 0), st, P);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
+    if (D == 8) {  // the twin of encode16_kernel
+        launch_enc16<true>(P, st);
+    } else {
+        const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
+        const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+        hipLaunchKernelGGL((encode_memonly_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P);
     }
-    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
-    const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (D == 8) hipLaunchKernelGGL((encode_memonly_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P);
-    else hipLaunchKernelGGL((encode_memonly_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2004,16 +2039,15 @@ int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, bool 
 }
 
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st) {
-    if (D == 8) hipLaunchKernelGGL(encode_fixup_kernel<8>, dim3(grid), dim3(256), 0, st, P);
-    else hipLaunchKernelGGL(encode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
+    if (D != 4) return -1;  // 8x8x8 replays inside encode16_kernel
+    hipLaunchKernelGGL(encode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 template <int PG>
 static void launch_dec_t(int D, uint32_t groups, const DecodeParams& P, hipStream_t st) {
-    static const size_t pad = lds_pad("DCT3D_DEC_LDS_PAD_KB", 0);
-    if (D == 8) hipLaunchKernelGGL((decode_kernel<8, PG>), dim3(groups), dim3(kBlock), pad, st, P);
-    else hipLaunchKernelGGL((decode_kernel<4, PG>), dim3(groups), dim3(kBlock), pad, st, P);
+    if (D == 8) hipLaunchKernelGGL((decode_kernel<8, PG>), dim3(groups), dim3(kBlock), 0, st, P);
+    else hipLaunchKernelGGL((decode_kernel<4, PG>), dim3(groups), dim3(kBlock), 0, st, P);
 }
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st) {

@@ -1,6 +1,6 @@
 // dct3d_runtime.cpp -- the C-ABI (include/dct3d.h): context, buffers, launches.
 //
-// Replaces the reference's per-call OpenCL setup (encoder.c:169-219, decoder.c:153-202,
+// Replaces the reference's per-call OpenCL setup (encoder.c:147-197, decoder.c:153-202,
 // OpenCLUtils.c:49-165) with a persistent context: the transform plan (DCT.initialize equivalent,
 // dct3d_plan.cpp) is built once and its fold tables uploaded once; device work buffers are grown on
 // demand and reused; everything runs on one HIP stream.  Errors are returned, never printed, never
@@ -67,6 +67,11 @@ struct dct3d_ctx {
     uint32_t flag_cap = 0;
     uint64_t last_units = 0;
     bool last_valid = false;
+    // in-wave replay (8x8x8 encode): two counter slots that alternate between calls; each launch zeroes
+    // the other slot for the next call, so a call needs no reset copy (zeroed once at creation)
+    DevBuf d_enc_counts;
+    int enc_slot = 0;
+    int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
@@ -200,6 +205,8 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
     }
     if (!rc) rc = upload(c->d_tabs, tabs, sizeof(tabs));
     if (!rc) rc = c->d_counters.grow(16);
+    if (!rc) rc = c->d_enc_counts.grow(16);
+    if (!rc && hipMemset(c->d_enc_counts.p, 0, 16) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc) {
         std::vector<uint16_t> diag(p.cs);
         diagonal_order(block_w, block_h, block_d, diag.data());
@@ -220,7 +227,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
-                      &c->d_cubes, &c->d_counters, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
+                      &c->d_cubes, &c->d_counters, &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egf_slot,
                       &c->d_egf_lbits, &c->d_egf_state})
@@ -303,9 +310,14 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
     st->n_units = c->last_units;
     if (!c->last_valid) return DCT3D_OK;
     uint32_t cnt[4] = {0, 0, 0, 0};
-    if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+    if (c->last_count_slot >= 0) {  // in-wave replay: the call's slot; no overflow path exists
+        if (hipMemcpyAsync(cnt, (uint32_t*)c->d_enc_counts.p + c->last_count_slot, 4, hipMemcpyDeviceToHost,
+                           c->stream) != hipSuccess)
+            return DCT3D_EDEVICE;
+    } else if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
         return DCT3D_EDEVICE;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return DCT3D_EDEVICE;
     st->n_flagged = cnt[0];
     st->n_overflow_cubes = cnt[1];
     return DCT3D_OK;
@@ -361,13 +373,19 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     c->last_valid = false;
+    c->last_count_slot = -1;
     if (n_cubes == 0) return DCT3D_OK;
-    rc = ensure_flag_buffers(c, n_cubes);
-    if (rc) return rc;
     const int D = c->bd;
+    // 8x8x8: one launch, uncertified coefficients replayed inside the wave; 8x8x4: flag list + fixup
+    const bool inwave = encode_replays_inwave(D);
+    if (!inwave) {
+        rc = ensure_flag_buffers(c, n_cubes);
+        if (rc) return rc;
+        if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    }
     const uint64_t plane = (uint64_t)w * h;
-    if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     EncodeParams P;
+    memset(&P, 0, sizeof(P));
     P.raster = d_raster;
     P.out = d_q;
     P.n_cubes = (uint32_t)n_cubes;
@@ -387,10 +405,29 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.counters = (unsigned int*)c->d_counters.p;
     P.flag_cap = c->flag_cap;
     P.cube_list = (uint32_t*)c->d_cubes.p;
+    P.ngroups = (const int32_t*)c->d_ngroups.p;
+    P.coef = (const double*)c->d_coef.p;
+    P.group_of = (const uint8_t*)c->d_group_of.p;
+    if (inwave) {
+        P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot;
+        P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1);
+    }
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (launch_encode(D, P, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[1], c->stream);
+    if (inwave) {
+        if (ev) {  // no fixup launch: the second event pair brackets nothing
+            (void)hipEventRecord(ev[2], c->stream);
+            (void)hipEventRecord(ev[3], c->stream);
+        }
+        c->last_count_slot = c->enc_slot;
+        c->enc_slot ^= 1;
+        c->last_units = n_cubes * (uint64_t)c->plan.cs;
+        c->last_valid = true;
+        if (d_dct) return forward_f64_raster(c, d_raster, w, h, n_cubes, d_dct);
+        return DCT3D_OK;
+    }
     FixupParams F;
     F.raster = d_raster;
     F.out = d_q;
@@ -442,6 +479,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     c->last_valid = false;
+    c->last_count_slot = -1;
     if (n_cubes == 0) return DCT3D_OK;
     rc = ensure_flag_buffers(c, n_cubes);
     if (rc) return rc;
@@ -662,6 +700,7 @@ static int cube_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* 
     }
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = false;  // no flag counters for the float path
+    c->last_count_slot = -1;
     return DCT3D_OK;
 }
 
@@ -775,6 +814,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     c->last_valid = false;
+    c->last_count_slot = -1;
     if (n_cubes == 0) return dct3d_eg_encode_dev(c, nullptr, 0, carry_byte, carry_bits, d_out, out_cap, total_bits);
     if (!d_out) return DCT3D_EINVAL;
     const int D = c->bd;
@@ -1094,6 +1134,7 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     c->last_valid = false;
+    c->last_count_slot = -1;
     if (end_bit) *end_bit = start_bit;
     if (n_cubes == 0) return DCT3D_OK;
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;

@@ -1,4 +1,4 @@
-/* codec.c -- encode()/decode(): the reference codec's pipeline (encoder.c:110-315,
+/* codec.c -- encode()/decode(): the reference codec's pipeline (encoder.c:88-293,
  * decoder.c:85-314) with the OpenCL block replaced by the libdct3d C-ABI.
  *
  * encode: per batch of stacks: fread -> dct3d_encode_stacks (fused DCT + quantisation on the GPU,
@@ -6,8 +6,8 @@
  * decode: inflate + Exp-Golomb + reorder per stack -> dct3d_decode_stacks (fused dequantisation +
  *         IDCT + clamp + truncation on the GPU) -> fwrite.
  * A stack is DCT_BLOCK_DEPTH frames; a short last stack is zero-filled (the reference reads
- * uninitialised bytes there, encoder.c:43-49).  Frames to encode are rounded up to whole stacks,
- * as in the reference loop (encoder.c:225).  Errors: printf + return 1 (the reference convention);
+ * uninitialised bytes there, encoder.c:21-27).  Frames to encode are rounded up to whole stacks,
+ * as in the reference loop (encoder.c:203).  Errors: printf + return 1 (the reference convention);
  * never exit(). */
 #include <stdint.h>
 #include <stdio.h>

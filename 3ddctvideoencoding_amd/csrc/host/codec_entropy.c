@@ -67,7 +67,7 @@ dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FI
     /* worst case: 63 bits per value (|v| < 2^31) -> 8 bytes per value */
     e->eg_cap = e->cubes * e->cs * 8 + 16;
     e->eg = (char *)calloc(e->eg_cap, 1);
-    if (!e->sp || !e->eg || deflateInit(&e->zs, Z_BEST_COMPRESSION) != Z_OK) {  /* encoder.c:158-161 */
+    if (!e->sp || !e->eg || deflateInit(&e->zs, Z_BEST_COMPRESSION) != Z_OK) {  /* encoder.c:136-139 */
         cubeUtils_deallocatePositions(e->sp);
         free(e->eg);
         free(e);
@@ -81,7 +81,7 @@ dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FI
 
 int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last) {
     if (e->finished) return -1;
-    /* applyExpGolombCoding (encoder.c:82-93): diagonal order inside each cube */
+    /* applyExpGolombCoding (encoder.c:60-71): diagonal order inside each cube */
     for (size_t c = 0; c < e->cubes; c++) {
         const int32_t *cube = q + c * e->cs;
         for (int i = 0; i < e->sp->length; i++) {
@@ -92,11 +92,11 @@ int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last) 
     const int size = e->st.bufferPosition;
     if (!is_last) {
         if (deflate_all(e, (const unsigned char *)e->eg, (size_t)size, Z_NO_FLUSH)) return -1;
-        expGolomb_freeBuffer(&e->st, size, 1);  /* keep the partial byte (encoder.c:290) */
+        expGolomb_freeBuffer(&e->st, size, 1);  /* keep the partial byte (encoder.c:268) */
         return 0;
     }
     e->finished = 1;
-    return deflate_all(e, (const unsigned char *)e->eg, (size_t)size + 1, Z_FINISH);  /* encoder.c:292 */
+    return deflate_all(e, (const unsigned char *)e->eg, (size_t)size + 1, Z_FINISH);  /* encoder.c:270 */
 }
 
 void dct3d_entropy_enc_carry(const dct3d_entropy_enc *e, uint8_t *byte, int *bits) {

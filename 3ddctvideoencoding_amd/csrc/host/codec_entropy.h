@@ -1,5 +1,5 @@
 /* codec_entropy.h -- the codec's entropy stage (diagonal-slice order -> signed Exp-Golomb -> zlib),
- * stream-compatible with the reference C codec (encoder.c:82-108,263-296 / decoder.c:61-83,209-244):
+ * stream-compatible with the reference C codec (encoder.c:60-86,241-274 / decoder.c:61-83,209-244):
  * one zlib stream (Z_BEST_COMPRESSION); per stack deflate(Z_NO_FLUSH) of the complete Exp-Golomb
  * bytes with the partial byte carried to the next stack; the last stack deflated with Z_FINISH
  * including its partial byte (+1).  Internal to libdct3dcodec (exported for the tests). */
@@ -19,14 +19,14 @@ typedef struct dct3d_entropy_dec dct3d_entropy_dec;
 
 /* sink: FILE* (out) or, if out == NULL, an internal growable memory buffer */
 dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FILE *out);
-/* q: one stack of cubes, cube-major int32; is_last selects Z_FINISH (encoder.c:288-293) */
+/* q: one stack of cubes, cube-major int32; is_last selects Z_FINISH (encoder.c:266-271) */
 int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last);
 /* the stream's current partial byte and the bits used in it (0..7): the carry for a stream built
  * elsewhere (the device Exp-Golomb stage, dct3d_encode_eg) */
 void dct3d_entropy_enc_carry(const dct3d_entropy_enc *e, uint8_t *byte, int *bits);
 /* appends an Exp-Golomb stream that starts with the carry above: total_bits bits (carry included) in
  * `bytes`; deflates its complete bytes (Z_NO_FLUSH) and keeps the partial byte, or, when is_last,
- * deflates them + the partial byte with Z_FINISH (encoder.c:285-296) */
+ * deflates them + the partial byte with Z_FINISH (encoder.c:263-274) */
 int dct3d_entropy_enc_push_stream(dct3d_entropy_enc *e, const unsigned char *bytes, uint64_t total_bits, int is_last);
 const unsigned char *dct3d_entropy_enc_memory(const dct3d_entropy_enc *e, size_t *len);
 void dct3d_entropy_enc_destroy(dct3d_entropy_enc *e);

@@ -1,4 +1,4 @@
-/* cube_io.c -- reference-signature host helpers (encoder.c:10-80, decoder.c:10-72 semantics). */
+/* cube_io.c -- reference-signature host helpers (encoder.c:10-58, decoder.c:10-72 semantics). */
 #include "cube_io.h"
 
 #include <math.h>

@@ -29,17 +29,20 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 CONFIGS = {
-    # name: (width, height, block_depth, stacks per GPU, direction)
+    # name: (width, height, block_depth, stacks per GPU, direction); stacks None = a fixed job split
+    # over the ranks (JOB_STACKS, strong scaling)
     "c2_encode_1080p": (1920, 1080, 8, 128, "encode"),
     "c3_decode_1080p": (1920, 1080, 8, 128, "decode"),
-    "c4_encode_4k": (3840, 2160, 8, 8, "encode"),
+    # BASELINE config 4: ONE job of 64 4K stacks, each rank encodes shard(64, N, rank) of them
+    # (contiguous ranges, Transform.java:88-104's per-cube independence; no data-path collective)
+    "c4_encode_4k": (3840, 2160, 8, None, "encode"),
     "c5_encode_1080p_d4": (1920, 1080, 4, 128, "encode"),
     "c6_decode_1080p_d4": (1920, 1080, 4, 128, "decode"),
     # encode to the Exp-Golomb stream: DCT + quantise + diagonal order + EG per step
     "c7_encode_eg_1080p": (1920, 1080, 8, 128, "encode_eg"),
     # decode from the Exp-Golomb stream: EG decode + dequantise + IDCT per step
     "c8_decode_eg_1080p": (1920, 1080, 8, 128, "decode_eg"),
-    # drop-in (A), the reference's own device block (encoder.c:231-276 / decoder.c:246-292): float
+    # drop-in (A), the reference's own device block (encoder.c:209-254 / decoder.c:246-292): float
     # cube-major in -> float cube-major out, DCT / IDCT + clamp, fp64 internal
     "c9_forward_f32_1080p": (1920, 1080, 8, 128, "forward_f32"),
     "c10_inverse_f32_1080p": (1920, 1080, 8, 128, "inverse_f32"),
@@ -54,16 +57,18 @@ WHAT = {
     "forward_f32": "drop-in (A) forward 3D DCT, f32 cube-major in/out",
     "inverse_f32": "drop-in (A) inverse 3D DCT + clamp, f32 cube-major in/out",
 }
+JOB_STACKS = {"c4_encode_4k": 64}
 HEADLINE_METRIC = "8×8×8 cubes/s (encode DCT+quant) on 1080p×8-frame stacks; % HBM roofline at 1/2/4/8 GPUs"
 
 
-def metric_name(direction: str, depth: int) -> str:
-    """BASELINE.json's metric for the encode configs at depth 8; the same form, naming what is timed,
-    for the other configs (they are parity / coverage lines, not the headline)."""
-    if direction == "encode" and depth == 8:
+def metric_name(direction: str, depth: int, width: int = 1920, height: int = 1080) -> str:
+    """BASELINE.json's metric for the 1080p encode at depth 8 (the headline, config 2); the same form,
+    naming what is timed, for the other configs (they are parity / coverage lines, not the headline)."""
+    if direction == "encode" and depth == 8 and (width, height) == (1920, 1080):
         return HEADLINE_METRIC
     unit = "8×8×8" if depth == 8 else "8×8×4"
-    return f"{unit} cubes/s ({WHAT[direction]}) on 1080p×{depth}-frame stacks; % HBM roofline"
+    size = "1080p" if (width, height) == (1920, 1080) else f"{width}×{height}"
+    return f"{unit} cubes/s ({WHAT[direction]}) on {size}×{depth}-frame stacks; % HBM roofline"
 
 
 def parse():
@@ -72,7 +77,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2_encode_1080p", choices=sorted(CONFIGS))
-    ap.add_argument("--stacks", type=int, default=None, help="override stacks per GPU")
+    ap.add_argument("--stacks", type=int, default=None, help="override stacks per GPU (weak scaling)")
+    ap.add_argument("--job-stacks", type=int, default=None,
+                    help="strong scaling: one job of this many stacks split over the ranks (sharding.shard); "
+                         "the default for c4_encode_4k is 64")
     ap.add_argument("--kind", default="ramp", choices=["ramp", "uniform"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -86,26 +94,74 @@ def parse():
     return ap.parse_args()
 
 
+def rank_stacks(config: str, stacks_override, job_override, world: int, rank: int):
+    """This rank's work: (first stack, stacks, job stacks or None, scaling).  Strong scaling (a job
+    config such as c4_encode_4k, or --job-stacks): one job of J stacks, rank r encodes its contiguous
+    shard sharding.shard(J, world, r).  Weak scaling: every rank encodes its own `stacks` stacks, rank r
+    the r-th slice of one long synthetic video."""
+    sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    per_gpu = CONFIGS[config][3]
+    job = job_override or (JOB_STACKS.get(config) if per_gpu is None and not stacks_override else None)
+    if job:
+        first, n = sharding.shard(job, world, rank)
+        return first, n, job, "strong"
+    n = stacks_override or per_gpu or JOB_STACKS.get(config, 1)
+    return rank * n, n, None, "weak"
+
+
+def java_available_processors() -> tuple[int, str]:
+    """What the reference's pool size, Runtime.getRuntime().availableProcessors() (Transform.java:63-64),
+    returns on this host: a container-aware JVM counts the CPUs in the process's affinity mask, capped by
+    the cgroup CPU quota (ceil(quota / period)) when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = "affinity"
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and txt and txt[0] != "max":
+            quota, period = int(txt[0]), int(txt[1])
+        elif path.endswith("cfs_quota_us") and txt and int(txt[0]) > 0:
+            quota = int(txt[0])
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().split()[0])
+        else:
+            continue
+        q = max(1, -(-quota // period))
+        if q < n:
+            n, src = q, "cgroup quota"
+        break
+    return n, src
+
+
 def cpu_baseline(width, height, depth, budget_s, kind):
     """Java-algorithm restatement (oracle/java_dct3d.c: grouped coefficients, memoised sums, one task
-    per cube on a fixed thread pool, Math.round quantisation) on a bounded sample of the workload."""
+    per cube on a fixed thread pool, Math.round quantisation) on a bounded sample of the workload.
+    Pool size = the reference's rule, availableProcessors() (Transform.java:63-64), except that an
+    explicit OMP_NUM_THREADS (the GPU box sets it to the CPU share granted per GPU, 16) caps it: the
+    machine's other cores belong to other jobs."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test infrastructure, used here only as the CPU baseline leg
 
     pkg = importlib.import_module("3ddctvideoencoding_amd")
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    avail, avail_src = java_available_processors()
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, env) if env > 0 else avail
     plan = oracle.Plan(8, 8, depth)
     cubes_per_stack = (width // 8) * (height // 8)
     done, t_total, stacks = 0, 0.0, 0
-    while t_total < budget_s and stacks < 16:
+    while t_total < budget_s and stacks < 64:
         fr = pkg.synthetic.frames(width, height, depth, frame0=stacks * depth, kind=kind)
         t0 = time.perf_counter()
         plan.encode_q(fr, threads=threads)
         t_total += time.perf_counter() - t0
         done += cubes_per_stack
         stacks += 1
-    return {"value": done / t_total, "unit": "cubes/s", "cores": threads, "kind": "port",
+    return {"value": done / t_total, "unit": "cubes/s", "cores": threads, "threads": threads,
+            "host_cores": os.cpu_count(), "available_processors": avail,
+            "pool_rule": f"availableProcessors() = {avail} ({avail_src})"
+                         + (f", capped by OMP_NUM_THREADS={env} (this box's CPU share)" if 0 < env < avail else ""),
+            "kind": "port",
             "sample": f"{stacks} x {width}x{height}x{depth} stack(s) ({done} cubes) through the restated Java "
                       f"DCT.run + Encoder quantisation, {threads} threads, {t_total:.1f} s"}
 
@@ -164,18 +220,19 @@ def measure_ceiling(ctx, torch, frames, q, reps, geom=None):
     return out
 
 
-def xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height, rank, world):
-    """Optional host-of-record distribution, timed apart from the hot path: rank 0 holds every rank's
-    stacks (the same synthetic content each rank generated for itself), scatters them over RCCL p2p
-    (xGMI), then gathers the quantised cubes back in stack order.  Both directions are verified: the
-    received frames equal the rank's own, the gathered cube sums equal the senders'."""
-    n_all = world * stacks
+def xgmi_leg(ctx, torch, dist, sharding, frames, q, n_all, depth, width, height, rank, world, kind):
+    """Optional host-of-record distribution, timed apart from the hot path: rank 0 holds the whole job
+    (the same synthetic content each rank generated for its own shard: one long video, frame0 = 0),
+    scatters every rank's stack range (sharding.shard) over RCCL p2p (xGMI), then gathers the quantised
+    cubes back in stack order.  Both directions are verified: the received frames equal the rank's own,
+    the gathered cube sums equal the senders'."""
+    first, count = sharding.shard(n_all, world, rank)
     stack_px = depth * height * width
-    stack_q = q.numel() // stacks
+    stack_q = (width // 8) * (height // 8) * 64 * depth
     full = None
     if rank == 0:
         full = torch.empty((n_all * depth, height, width), dtype=torch.uint8, device="cuda")
-        ctx.fill_synthetic_dev(full, width, height, n_all * depth, frame0=0)
+        ctx.fill_synthetic_dev(full, width, height, n_all * depth, frame0=0, kind=kind)
     recv = torch.empty_like(frames)
     torch.cuda.synchronize()
 
@@ -196,11 +253,11 @@ def xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height
     gathered = torch.empty((n_all * stack_q,), dtype=torch.int32, device="cuda") if rank == 0 else None
     t_ga = timed(lambda: sharding.gather_stacks(q, gathered, n_all, stack_q, rank, world))
     sums = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-    dist.all_gather(sums, q.sum(dtype=torch.int64).view(1))
+    dist.all_gather(sums, q[:count * stack_q].sum(dtype=torch.int64).view(1))
     if rank == 0:
-        g = gathered.view(world, -1)
         for r in range(world):
-            if int(g[r].sum(dtype=torch.int64).item()) != int(sums[r].item()):
+            f, c = sharding.shard(n_all, world, r)
+            if int(gathered[f * stack_q:(f + c) * stack_q].sum(dtype=torch.int64).item()) != int(sums[r].item()):
                 ok.zero_()
     del gathered
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -212,13 +269,13 @@ def xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height
 def main():
     a = parse()
     width, height, depth, stacks, direction = CONFIGS[a.config]
-    if a.stacks:
-        stacks = a.stacks
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus and world != 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
+    first, stacks, job_stacks, scaling = rank_stacks(a.config, a.stacks, a.job_stacks, world, rank)
 
     import torch
 
@@ -248,10 +305,10 @@ def main():
 
     n_cubes = ctx.n_cubes(width, height, stacks)
     cs = 64 * depth
-    frames = torch.empty((stacks * depth, height, width), dtype=torch.uint8, device="cuda")
+    frames = torch.empty((max(1, stacks) * depth, height, width), dtype=torch.uint8, device="cuda")
     # each rank encodes different content (its own slice of one long synthetic video)
-    ctx.fill_synthetic_dev(frames, width, height, stacks * depth, frame0=rank * stacks * depth, kind=a.kind)
-    q = torch.empty((n_cubes * cs,), dtype=torch.int32, device="cuda")
+    ctx.fill_synthetic_dev(frames, width, height, stacks * depth, frame0=first * depth, kind=a.kind)
+    q = torch.empty((max(1, n_cubes) * cs,), dtype=torch.int32, device="cuda")
     eg_info = {}
     if direction == "decode":
         ctx.encode_stacks_dev(frames, width, height, stacks, q)  # input of the decode = encoder output
@@ -332,58 +389,78 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    # device-side time of the whole timed region on the bench stream (every launch of every step and
+    # the gaps between them): the roofline basis, the same interval as `value`'s host clock
+    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev_a.record()
     for _ in range(a.steps):
         step()
+    ev_b.record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    dev_step_ms = ev_a.elapsed_time(ev_b) / a.steps
     st = ctx.stats()
     ctx.set_profiling(False)
     round_trip = None
-    if direction in ("decode", "decode_eg"):  # the codec's round trip on this GPU's frames
+    if direction in ("decode", "decode_eg") and stacks:  # the codec's round trip
         d = out.to(torch.int16) - frames.to(torch.int16)
         mse = float((d.to(torch.float64) ** 2).mean())
         round_trip = {"vs": "encoder input frames (lossy: quantisation); bit-exactness against the Java-semantics "
                             "decode is pinned by tests/test_gpu_parity.py",
                       "max_abs_err": int(d.abs().max()), "mean_abs_err": float(d.abs().to(torch.float64).mean()),
                       "psnr_db": (10.0 * math.log10(255.0 ** 2 / mse)) if mse > 0 else None}
-    ceiling = None if a.no_ceiling or q is None else measure_ceiling(
+    ceiling = None if a.no_ceiling or q is None or not stacks else measure_ceiling(
         ctx, torch, frames, q, max(3, a.steps // 2),
         geom=(width, height, stacks, cs * 5) if direction == "encode" else None)
-    sharding = importlib.import_module("3ddctvideoencoding_amd.sharding")
-    elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
-    xgmi = None
-    if a.xgmi and dist is not None and direction == "encode" and os.environ.get("DCT3D_BENCH_BACKEND", "nccl") == "nccl":
-        xgmi = xgmi_leg(ctx, torch, dist, sharding, frames, q, stacks, depth, width, height, rank, world)
 
-    ms_per_step = elapsed * 1e3 / a.steps
-    value = total_cubes * a.steps / elapsed
     bytes_per_cube = cs * (1 + 4)  # u8 in + int32 out (encode) / int32 in + u8 out (decode)
     if direction in ("forward_f32", "inverse_f32"):
         bytes_per_cube = cs * (4 + 4)  # f32 in + f32 out (4,096 B per cube)
     fused = direction == "encode_eg" and not a.eg_two_step
     if fused:  # u8 in + the cube's share of the coded stream, lane bit counts and segment totals out
-        bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes + (64 * 2 + 4) / 8
-    kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
-    fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
-    achieved = n_cubes * bytes_per_cube / (kernel_ms * 1e-3) / 1e9
-    if ceiling and "encode_memonly_GBs" in ceiling:  # the kernel against its own traffic without compute
-        ceiling["kernel_vs_memonly"] = achieved / ceiling["encode_memonly_GBs"]
+        bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes) + (64 * 2 + 4) / 8
     fused_dec = direction == "decode_eg" and not a.eg_two_step
     if fused_dec:  # the cube's share of the stream in, u8 out
-        bytes_per_cube = cs + eg_info["bits"] / 8 / n_cubes
+        bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes)
+    kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
+    fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
+    alg_bytes = n_cubes * bytes_per_cube
+    achieved = alg_bytes / (dev_step_ms * 1e-3) / 1e9 if n_cubes else 0.0       # step basis
+    kernel_achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    if ceiling and "encode_memonly_GBs" in ceiling:  # the kernel against its own traffic without compute
+        ceiling["kernel_vs_memonly"] = kernel_achieved / ceiling["encode_memonly_GBs"]
+        ceiling["step_vs_memonly"] = achieved / ceiling["encode_memonly_GBs"]
     kname = ("decode_eg_kernel" if fused_dec else "decode_kernel") if direction in ("decode", "decode_eg") else (
-        "encode_eg_kernel" if fused else "encode_kernel")
+        "encode_eg_kernel" if fused else ("encode16_kernel" if depth == 8 else "encode_kernel"))
     if direction in ("forward_f32", "inverse_f32"):
         kname = "cube_f32_kernel"
-    if kname == "encode_kernel" and depth == 8 and os.environ.get("DCT3D_ENC_VARIANT", "6") == "6":
-        kname = "encode16_kernel"  # the 8x8x8 default: 16 lanes per cube (not templated on the depth)
-    traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not a.stacks else (None, None)
+    step_kernels = {"encode": [kname] if depth == 8 else ["memset (counter reset)", kname, "encode_fixup_kernel"],
+                    "decode": ["memset (counter reset)", kname, "decode_fixup_kernel"]}.get(direction, [kname])
+    traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not (a.stacks or a.job_stacks) else (None, None)
+
+    # per-rank record (strong scaling: shards differ in size; the job rate is total cubes / max time)
+    per_rank = None
+    if dist:
+        mine = torch.tensor([float(rank), float(stacks), float(n_cubes), dev_step_ms, achieved / HBM_PEAK_GBS],
+                            dtype=torch.float64, device="cuda")
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [{"rank": int(r[0]), "stacks": int(r[1]), "cubes": int(r[2]), "device_ms_per_step": float(r[3]),
+                     "frac": float(r[4])} for r in (x.tolist() for x in allr)]
+    elapsed, total_cubes = sharding.reduce_timing(elapsed, n_cubes, device="cuda")  # max time, summed units
+    xgmi = None
+    if a.xgmi and dist is not None and direction == "encode" and os.environ.get("DCT3D_BENCH_BACKEND", "nccl") == "nccl":
+        xgmi = xgmi_leg(ctx, torch, dist, sharding, frames[:stacks * depth], q, job_stacks or world * stacks,
+                        depth, width, height, rank, world, a.kind)
+
+    ms_per_step = elapsed * 1e3 / a.steps
+    value = total_cubes * a.steps / elapsed
     unit_name = "8x8x8" if depth == 8 else "8x8x4"
     res = {
-        "metric": metric_name(direction, depth),
+        "metric": metric_name(direction, depth, width, height),
         "value": value,
         "unit": "cubes/s",
         "n_gpus": world,
@@ -391,16 +468,19 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64" if direction in ("decode", "decode_eg", "forward_f32", "inverse_f32") else "f32",
         "data": "synthetic",
         "config": {
             "workload": f"{width}x{height} grayscale, {depth}-frame stacks, "
                         f"{WHAT[direction]}"
-                        f" ({unit_name} cubes), {stacks} device-resident stacks per GPU per step",
+                        f" ({unit_name} cubes), "
+                        + (f"one job of {job_stacks} device-resident stacks split over {world} GPU(s)" if job_stacks
+                           else f"{stacks} device-resident stacks per GPU per step"),
             "name": a.config,
-            "stacks_per_gpu": stacks,
+            "stacks_per_gpu": stacks if not job_stacks else None,
+            "job_stacks": job_stacks,
             "cubes_per_gpu_step": n_cubes,
             "content": a.kind,
             "parallelism": f"dp{world} (stacks sharded, no data-path collective)",
@@ -411,13 +491,18 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,  # HBM bytes per launch (PMC), compare with algorithmic_bytes
+            "basis": "algorithmic bytes of one step / device time per step (HIP events around the timed "
+                     "region on the bench stream: every launch of the step, " + " + ".join(step_kernels) + ")",
+            "traffic": traffic,  # HBM bytes per launch of the main kernel (PMC), compare with algorithmic_bytes
             "traffic_source": traffic_src,
-            "algorithmic_bytes": n_cubes * bytes_per_cube,
+            "algorithmic_bytes": alg_bytes,
+            "bytes_per_cube": bytes_per_cube,
+            "device_ms_per_step": dev_step_ms,
             "kernel": kname,
             "kernel_ms": kernel_ms,
             "fixup_ms": fixup_ms,
-            "bytes_per_cube": bytes_per_cube,
+            "kernel_only_achieved": kernel_achieved,
+            "kernel_only_frac": kernel_achieved / HBM_PEAK_GBS,
         },
         "ceiling": ceiling,
         "flagged_units_last_step": st["n_flagged"],
@@ -426,11 +511,13 @@ def main():
         "eg_stage": None if direction not in ("encode_eg", "decode_eg") else {
             "path": ("fused" if fused_dec else "two-step") if direction == "decode_eg" else ("fused" if fused else "two-step"),
             "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
-            "bits_per_value": eg_info["bits"] / (n_cubes * cs),
+            "bits_per_value": eg_info["bits"] / (max(1, n_cubes) * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
         "round_trip": round_trip,
         "cpu_baseline": None,
     }
+    if per_rank is not None:
+        res["per_rank"] = per_rank
     if xgmi is not None:
         res["xgmi"] = xgmi
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-/* encoder.c:110 / decoder.c:85.  platformIndex is the reference's 1-based device selector
+/* encoder.c:88 / decoder.c:85.  platformIndex is the reference's 1-based device selector
  * (main.c:33-37); here it selects HIP device (platformIndex - 1).  Returns 0 on success, 1 on
  * failure after printing the reason (the reference's convention). */
 int encode(char *inputFileName, char *outputFileName, int width, int height, int framesToEncode, int platformIndex);

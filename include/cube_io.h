@@ -1,6 +1,6 @@
 /*
  * cube_io.h -- host-side cube pack/unpack and (de)quantisation helpers with the reference C codec's
- * signatures and semantics (encoder.c:10-80, decoder.c:10-72), kept for callers of the drop-in (A)
+ * signatures and semantics (encoder.c:10-58, decoder.c:10-72), kept for callers of the drop-in (A)
  * path (dct3d_forward_f32 / dct3d_inverse_f32).  The fused path (dct3d_encode_stacks /
  * dct3d_decode_stacks) does all of this on the device.
  *
@@ -24,7 +24,11 @@
 extern "C" {
 #endif
 
-/* returns the number of bytes actually read (< width*height*depth at end of file) */
+/* Difference from the reference: readCubes / writeCubes return size_t where the reference returns
+ * void (encoder.c:10, decoder.c:10).  readCubes returns the number of raw bytes actually read
+ * (< width*height*depth at end of file), writeCubes the number of bytes written.  A caller written
+ * against the reference's prototypes (ignoring the result) compiles and links unchanged: on every
+ * C ABI in use the return register is simply not read, and no argument changes. */
 size_t readCubes(FILE *inputFile, float *data, int width, int height);
 size_t writeCubes(FILE *outputFile, float *data, int width, int height);
 void applyQuantization(float *dctCoeff, size_t bufferSize);

@@ -4,10 +4,10 @@
  * Drop-in boundary for julianopiccoli/3dDCTVideoEncoding's per-stack device block.  The reference
  * C codec (3d-DCT-video-encoding-OpenCL/) does, per 8-frame stack:
  *     readCubes -> clEnqueueWriteBuffer -> dct_calculate_partial_sums -> dct_aggregate_partial_sums
- *     -> clEnqueueReadBuffer -> applyQuantization                       (encoder.c:228-282)
+ *     -> clEnqueueReadBuffer -> applyQuantization                       (encoder.c:206-260)
  *     applyDequantization -> clEnqueueWriteBuffer -> idct_calculate_partial_sums
  *     -> idct_aggregate_partial_sums -> clEnqueueReadBuffer -> writeCubes (decoder.c:246-295)
- * after a per-call OpenCL setup (encoder.c:169-219, decoder.c:153-202, OpenCLUtils.c:49-165).
+ * after a per-call OpenCL setup (encoder.c:147-197, decoder.c:153-202, OpenCLUtils.c:49-165).
  * Each entry point below names the reference region it replaces.
  *
  * Conventions (all entry points):
@@ -15,10 +15,10 @@
  *     (the reference printf()s and returns 1, or exit(1)s inside OpenCLUtils.c; this library never
  *     prints and never exits -- the codec layer above prints, see codec.h);
  *   - a context owns its device buffers and its HIP stream (the reference creates its OpenCL objects
- *     per call and never releases them, encoder.c:187-219); one context per device, one host
+ *     per call and never releases them, encoder.c:165-197); one context per device, one host
  *     thread per context (a context is not thread-safe);
  *   - host-pointer entry points are synchronous on return (the reference's blocking
- *     clEnqueueWrite/ReadBuffer, encoder.c:231,276); *_dev entry points take device pointers and
+ *     clEnqueueWrite/ReadBuffer, encoder.c:209,254); *_dev entry points take device pointers and
  *     are asynchronous on the context stream (use dct3d_synchronize).  The context's own stream is a
  *     blocking stream (ordered with the legacy default stream); dct3d_ctx_set_stream selects another;
  *   - frame width must be a multiple of the block width and height of the block height
@@ -26,10 +26,10 @@
  *     DCT3D_EINVAL.
  *
  * Layouts:
- *   raster  : u8 frames, frame-major, row-major (the raw grayscale file format, encoder.c:43-49);
+ *   raster  : u8 frames, frame-major, row-major (the raw grayscale file format, encoder.c:21-27);
  *             a "stack" is DCT_BLOCK_DEPTH consecutive frames.
  *   cubes   : cube-major: for each stack, block-row by, block-col bx, then (z, y, x) inside the cube
- *             (readCubes order, encoder.c:51-63; Java Encoder.java:75-89).
+ *             (readCubes order, encoder.c:29-41; Java Encoder.java:75-89).
  *
  * Numerics (parity target = the reference Java codec, BASELINE.json north_star):
  *   - dct3d_encode_stacks*: quantised int32 coefficients equal to the Java path
@@ -102,7 +102,7 @@ const char *dct3d_strerror(int code);
 
 /* Replaces the per-call OpenCL setup: getDeviceId/getMaxWorkGroupSize (OpenCLUtils.c:69-104),
  * clCreateContext/buildKernel/clCreateBuffer/clCreateCommandQueue/clCreateKernel
- * (encoder.c:180-219, decoder.c:163-202).  `device` is a 0-based HIP ordinal (the codec layer
+ * (encoder.c:158-197, decoder.c:163-202).  `device` is a 0-based HIP ordinal (the codec layer
  * maps the reference's 1-based platformIndex, main.c:33-37).  Block dims are the codec.h macros
  * DCT_BLOCK_WIDTH/HEIGHT/DEPTH (codec.h:11-13); supported: 8 x 8 x 8 and 8 x 8 x 4. */
 int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ctx **out);
@@ -121,7 +121,7 @@ int dct3d_reset_timers(dct3d_ctx *ctx);
 
 /* ---------------------------------------------------------------------------------------------
  * Native fused path (B): replaces readCubes + H2D + dct kernels + D2H + applyQuantization
- * (encoder.c:228-282) for n_stacks consecutive stacks.
+ * (encoder.c:206-260) for n_stacks consecutive stacks.
  *   raster : n_stacks * block_d frames of width*height u8
  *   q_cubes: n_stacks * (width/bw) * (height/bh) cubes of bw*bh*bd int32 (cube-major)
  *   dct_opt: optional (may be NULL) fp64 DCT coefficients, same cube-major layout (the Java
@@ -140,7 +140,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx *ctx, const int32_t *d_q_cubes, int width,
 
 /* ---------------------------------------------------------------------------------------------
  * Reference-faithful drop-in (A): the exact data flow of the OpenCL block, float cube-major in,
- * float cube-major out (kernelInputData -> kernelOutputData, encoder.c:187-276 / decoder.c:
+ * float cube-major out (kernelInputData -> kernelOutputData, encoder.c:165-254 / decoder.c:
  * 170-292).  The caller keeps readCubes/applyQuantization (forward) and applyDequantization/
  * writeCubes (inverse) on the host, exactly as the reference does.
  *   dct3d_forward_f32: orthonormal 3D DCT-II of each cube (dct_* kernels, 3dDCT.cl:43-143)
@@ -188,13 +188,13 @@ int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width,
 int dct3d_eg_encode_dev(dct3d_ctx *ctx, const int32_t *d_q, uint64_t n_cubes, uint8_t carry_byte, int carry_bits,
                         uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
 
-/* Host raster in, Exp-Golomb stream kept on the device: encoder.c:228-296 up to (not including) the
+/* Host raster in, Exp-Golomb stream kept on the device: encoder.c:206-274 up to (not including) the
  * deflate -- readCubes + DCT + quantisation + applyExpGolombCoding for n_stacks stacks, one H2D copy
  * of the raw bytes.  *total_bits as above; fetch the bytes with dct3d_eg_fetch. */
 int dct3d_encode_eg(dct3d_ctx *ctx, const uint8_t *raster, int width, int height, int n_stacks, uint8_t carry_byte,
                     int carry_bits, uint64_t *total_bits);
 
-/* Device raster in, device stream out, fused: encoder.c:228-296 up to the deflate
+/* Device raster in, device stream out, fused: encoder.c:206-274 up to the deflate
  * (readCubes + DCT + quantisation + applyExpGolombCoding) for n_stacks stacks of d_raster, without
  * the int32 cube-major intermediate -- uncertified coefficients are replayed exactly inside the
  * transform kernel, and each wave codes its 8 cubes straight into the stream.  The stream format,

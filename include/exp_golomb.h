@@ -3,7 +3,7 @@
  * (replaces 3d-DCT-video-encoding-OpenCL/ExpGolomb.h:4-16; Java ExpGolombWriter/Reader.java).
  * Mapping v <= 0 -> -2v, v > 0 -> 2v - 1, then +1, MSB first.  bitPosition counts the free bits of
  * the current byte (8 = empty).  Unlike the reference, createStream zeroes the first byte (the
- * reference ORs into an uninitialised malloc'd byte, ExpGolomb.c:24-30 + encoder.c:155).
+ * reference ORs into an uninitialised malloc'd byte, ExpGolomb.c:24-30 + encoder.c:133).
  */
 #ifndef DCT3D_EXP_GOLOMB_H_
 #define DCT3D_EXP_GOLOMB_H_

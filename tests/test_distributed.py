@@ -113,3 +113,22 @@ def test_scatter_gather_stacks_gloo(tmp_path, world):
         f, c = sh.shard(7, world, r)
         exp[f * 40:(f + c) * 40] += r
     assert np.array_equal(back, exp)
+
+
+def test_bench_job_split():
+    """bench.py's per-rank work: config 4 is ONE job of 64 4K stacks split over the ranks (strong
+    scaling, contiguous shards covering the job exactly once); config 2 gives every rank its own 128
+    stacks (weak scaling), rank r the r-th slice of one video."""
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module("bench")
+    for world in (1, 2, 4, 8, 3):
+        parts = [bench.rank_stacks("c4_encode_4k", None, None, world, r) for r in range(world)]
+        assert all(p[2] == 64 and p[3] == "strong" for p in parts)
+        assert sum(p[1] for p in parts) == 64
+        assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+        if 64 % world == 0:
+            assert all(p[1] == 64 // world for p in parts)
+        w = [bench.rank_stacks("c2_encode_1080p", None, None, world, r) for r in range(world)]
+        assert all(p == (r * 128, 128, None, "weak") for r, p in enumerate(w))
+    assert bench.rank_stacks("c4_encode_4k", 8, None, 2, 1) == (8, 8, None, "weak")      # --stacks: weak
+    assert bench.rank_stacks("c2_encode_1080p", None, 10, 4, 3) == (8, 2, 10, "strong")  # --job-stacks

@@ -1,6 +1,6 @@
 """GPU: the fused encode + Exp-Golomb path (dct3d_encode_eg_dev).
 
-The stream must be the reference's (encoder.c:228-296 up to the deflate: DCT + quantisation +
+The stream must be the reference's (encoder.c:206-274 up to the deflate: DCT + quantisation +
 diagonal-slice order + signed order-0 Exp-Golomb, one continuous bitstream carrying the partial byte)
 bit for bit.  Expected streams: the oracle's quantised cubes (plan.encode_q, the restated Java
 DCT.java / Encoder.java) through the oracle's Exp-Golomb writer at sizes the oracle finishes in

@@ -3,7 +3,7 @@ codec_entropy.c) against the oracle and against the reference's own C helpers (o
 
 The entropy stage (diagonal order -> Exp-Golomb -> zlib) is replayed with the reference encoder's
 own applyExpGolombCoding + applyZlibCompression + expGolomb_freeBuffer call sequence
-(encoder.c:263-296) and must produce the same .bin bytes.
+(encoder.c:241-274) and must produce the same .bin bytes.
 """
 import ctypes as C
 import os
@@ -100,7 +100,7 @@ def _ref_or_skip():
 
 
 def reference_entropy_encode(q, w, h, stacks, depth):
-    """encoder.c:143-296's entropy stage, driven with the reference's own functions."""
+    """encoder.c:121-274's entropy stage, driven with the reference's own functions."""
     R = _ref_or_skip()
     z = C.CDLL("libz.so.1")
     z.zlibVersion.restype = C.c_char_p
