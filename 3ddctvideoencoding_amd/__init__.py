@@ -27,11 +27,14 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
 DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
+# test / diagnostic options (include/dct3d.h, Context.set_option)
+(DCT3D_OPT_FLAG_CAP, DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_SINGLE_PASS, DCT3D_OPT_EG_TWO_STEP,
+ DCT3D_OPT_EG_NO_RESOLVE) = 1, 2, 3, 4, 5, 6
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "dct3d_abi_version", "dct3d_strerror", "dct3d_ctx_create", "dct3d_ctx_destroy",
-    "dct3d_ctx_set_stream", "dct3d_ctx_set_profiling", "dct3d_synchronize", "dct3d_get_stats",
+    "dct3d_ctx_set_stream", "dct3d_ctx_set_option", "dct3d_ctx_set_profiling", "dct3d_synchronize", "dct3d_get_stats",
     "dct3d_reset_timers",
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
@@ -50,12 +53,13 @@ class Dct3dError(RuntimeError):
 class PlanInfo(C.Structure):
     _fields_ = [("cube_size", C.c_int), ("n_mults", C.c_int), ("treeified", C.c_int), ("coef_dc", C.c_double),
                 ("dec_G", C.c_double), ("dec_E", C.c_double), ("enc_rstep", C.c_float * 32),
-                ("enc_G", C.c_float * 32), ("enc_E", C.c_float * 32)]
+                ("enc_G", C.c_float * 32), ("enc_E", C.c_float * 32), ("enc_thr64", C.c_double * 32)]
 
 
 class Stats(C.Structure):
     _fields_ = [("n_units", C.c_uint64), ("n_flagged", C.c_uint64), ("n_overflow_cubes", C.c_uint64),
-                ("n_timed", C.c_uint64), ("kernel_ms_total", C.c_double), ("fixup_ms_total", C.c_double)]
+                ("n_timed", C.c_uint64), ("kernel_ms_total", C.c_double), ("fixup_ms_total", C.c_double),
+                ("n_rechecked", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -87,6 +91,7 @@ def lib() -> C.CDLL:
         L.dct3d_ctx_destroy.restype = None
         L.dct3d_ctx_set_stream.argtypes = [vp, vp]
         L.dct3d_ctx_set_profiling.argtypes = [vp, i32]
+        L.dct3d_ctx_set_option.argtypes = [vp, i32, C.c_double]
         L.dct3d_synchronize.argtypes = [vp]
         L.dct3d_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.dct3d_reset_timers.argtypes = [vp]
@@ -152,7 +157,7 @@ def plan_query(block_w: int = 8, block_h: int = 8, block_d: int = 8) -> dict:
     return {"cube_size": info.cube_size, "n_mults": info.n_mults, "treeified": bool(info.treeified),
             "coef_dc": info.coef_dc, "dec_G": info.dec_G, "dec_E": info.dec_E,
             "enc_rstep": np.array(info.enc_rstep[:]), "enc_G": np.array(info.enc_G[:]),
-            "enc_E": np.array(info.enc_E[:]), "ngroups": ng, "coef": coef.reshape(cs, 64),
+            "enc_E": np.array(info.enc_E[:]), "enc_thr64": np.array(info.enc_thr64[:]), "ngroups": ng, "coef": coef.reshape(cs, 64),
             "group_of": gof.reshape(cs, cs), "enc_K": K}
 
 
@@ -202,6 +207,11 @@ class Context:
         """Run on an external hipStream_t.  None or 0 (e.g. torch's default stream, whose handle is 0)
         selects the context's own stream -- use a non-default stream to share one with a framework."""
         _check(lib().dct3d_ctx_set_stream(self._h, hip_stream or None), "dct3d_ctx_set_stream")
+
+    def set_option(self, option: int, value: float) -> None:
+        """Test / diagnostic option (DCT3D_OPT_*): changes how later calls reach their (identical)
+        results, e.g. to drive a rare path.  0 restores the default."""
+        _check(lib().dct3d_ctx_set_option(self._h, option, float(value)), "dct3d_ctx_set_option")
 
     def set_profiling(self, on: bool) -> None:
         _check(lib().dct3d_ctx_set_profiling(self._h, 1 if on else 0), "dct3d_ctx_set_profiling")

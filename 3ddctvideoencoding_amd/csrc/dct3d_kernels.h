@@ -8,6 +8,10 @@
 namespace dct3d {
 
 constexpr int kMaxGroupsDev = 64;  // == kMaxGroups in dct3d_plan.h; one LDS slot per lane
+// Per-call counters of the in-wave paths are spread over kCountSpread words per counter (a block adds
+// to word blockIdx & (kCountSpread - 1)): 10^5 same-address atomics per call serialise at the L2
+// (~12 ns each, longer than the whole kernel); the host sums the words.
+constexpr int kCountSpread = 512;
 
 // n / d for n < 2^31 as one 32x32->64 multiply and a shift (Granlund-Montgomery: s = 31 + ceil(log2 d),
 // m = ceil(2^s / d) < 2^32 gives floor(n m / 2^s) = floor(n / d) for every n < 2^31); set_fast_div
@@ -40,8 +44,11 @@ struct EncodeParams {
     const int32_t* ngroups;    // [cs] exact replay tables (as FixupParams)
     const double* coef;        // [cs * kMaxGroupsDev]
     const uint8_t* group_of;   // [cs * cs]
-    unsigned int* replay_count;  // this call's counter slot (coefficients replayed), or nullptr
-    unsigned int* replay_clear;  // the other slot: zeroed by the launch for the next call, or nullptr
+    unsigned int* replay_count;  // this call's counter slot: [0, S) Java-fold replays, [S, 2S) fp64
+                                 // settlements (S = kCountSpread words each), or nullptr
+    unsigned int* replay_clear;  // the other slot (2S words): zeroed by block 0 for the next call
+    const double* tab64;       // second certificate: [64] fp64 basis [k][n], [32] thresholds per s
+    uint32_t recheck;          // 1: run the second certificate (0: test option, all open -> Java fold)
 };
 
 struct FixupParams {

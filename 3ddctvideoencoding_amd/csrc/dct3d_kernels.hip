@@ -727,16 +727,95 @@ __device__ __forceinline__ void e16_flag_pos(uint32_t fm, int src, uint32_t cube
     kk = (uint32_t)((sk * 8 + (bit >> 2)) * 8 + 4 * sh + (bit & 3));
 }
 
+// Second certificate (8x8x8 rare path): every coefficient the fp32 certificate left open (fm) is
+// re-evaluated in fp64 from the cube's bytes, one coefficient per cube per round (a cube's 16 lanes
+// together; the wave's 4 cubes in parallel):
+//   v64 = sum over the cube's lanes (c, k, h) of  b[ky][k] * sum_e b[kz][4h+e] * sum_x x[4h+e][k][x] b[kx][x]
+// (b = the fp64 basis, fma chains, an xor-butterfly sum: every lane of the cube gets the same bits).
+// q64 = v64 / step is settled iff |q64 - rint(q64)| < thr64[s]: then Math.round of Java's value is
+// rint(q64) (bound: dct3d_plan.cpp, "second certificate").  What stays open is returned in fm for the
+// exact Java fold; nset counts the settled ones (owner lanes).
+// Timing: the rows (raw, again: L2) and the tables (bv, tv) were loaded before the wave's stores and
+// arrive while those drain; this runs after the stores, and the owning lane writes a settled value
+// over the provisional one once the wave's stores are complete (vmcnt(0): the same word was stored by
+// another lane of the wave).  Register pressure stays with the main path's 72 VGPRs.  s_b: the block's
+// copy of the tables ([64] basis, [32] thresholds), written by every wave that takes this path
+// (identical bits) and read only after its own writes.
+__device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2 (&raw)[4], double bv, double tv,
+                                              double* s_b, int lane, uint32_t cube0, uint32_t& fm, uint32_t& nset) {
+    constexpr int CS = 512;
+    const int k = lane & 7, h = (lane >> 4) & 1;
+    s_b[lane] = bv;
+    if (lane < 32) s_b[64 + lane] = tv;
+    wave_lds_sync();
+    const int base = (lane & 32) + (lane & 8);
+    const uint64_t cmask = (0xFFull << base) | (0xFFull << (base + 16));  // this lane's cube
+    uint32_t open = 0u;
+    nset = 0u;
+    for (;;) {
+        const uint64_t any = __ballot(fm != 0u);
+        if (any == 0ull) break;
+        const uint64_t mine = any & cmask;
+        const int src = mine ? (int)__builtin_ctzll(mine) : lane;
+        const int bit = __shfl(fm ? (int)__builtin_ctz(fm) : 0, src, 64);
+        const int kz = src & 7, ky = bit >> 2, kx = 4 * ((src >> 4) & 1) + (bit & 3);
+        const double* bx = s_b + kx * 8;
+        double t = 0.0;
+#pragma unroll 1
+        for (int e = 0; e < 4; e += 2) {  // two rows' chains side by side
+            uint32_t w[4] = {raw[e].x, raw[e + 1].x, raw[e].y, raw[e + 1].y};
+            double r0 = 0.0, r1 = 0.0;
+#pragma unroll
+            for (int x = 0; x < 8; x++) {
+                const int i = x >> 2;
+                const double b = bx[x];
+                r0 = __fma_rn((double)(w[2 * i] & 0xFFu), b, r0);
+                r1 = __fma_rn((double)(w[2 * i + 1] & 0xFFu), b, r1);
+                w[2 * i] >>= 8;
+                w[2 * i + 1] >>= 8;
+                asm volatile("" : "+v"(w[2 * i]), "+v"(w[2 * i + 1]));  // conversions stay in the chains
+            }
+            t = __fma_rn(r0, s_b[kz * 8 + 4 * h + e], t);
+            t = __fma_rn(r1, s_b[kz * 8 + 4 * h + e + 1], t);
+        }
+        t = __dmul_rn(t, s_b[ky * 8 + k]);
+#pragma unroll
+        for (int o = 1; o <= 16; o <<= 1) {
+            if (o == 8) continue;  // the cube's lanes: k bits (1, 2, 4) and h (16)
+            t = __dadd_rn(t, __shfl_xor(t, o, 64));
+        }
+        if (mine != 0ull && lane == src) {
+            const int s = kz + ky + kx;
+            const double q = __ddiv_rn(t, (double)(5 * s));  // s >= 1: the DC is never open
+            const double n = __builtin_rint(q);
+            if (__builtin_fabs(q - n) < s_b[64 + s]) {
+                const uint32_t cube = cube0 + (lane >> 5) * 2 + ((lane & 15) >> 3);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                P.out[(size_t)cube * CS + (kz * 8 + ky) * 8 + kx] = (int32_t)n;
+                nset++;
+            } else {
+                open |= 1u << bit;
+            }
+            fm &= fm - 1u;  // its lowest bit is `bit`
+        }
+    }
+    fm = open;
+    wave_lds_sync();
+}
+
 // MEM (dct3d_encode_memonly_dev, DIAGNOSTIC: the output is NOT a DCT): the same loads, staging and
 // stores with the transform, quantisation and certification replaced by a few integer ops.
 // One launch is the whole encode: no flag list, no counter reset, no fixup launch.  Block 0 zeroes the
-// next call's replay counter slot (P.replay_clear; the two slots alternate between calls).
+// next call's counter slot (P.replay_clear; the two slots alternate between calls).  7 waves per SIMD
+// (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (they
+// spill a few registers to scratch instead, off the main path).
 static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the wave's region");
 template <bool NT, bool MEM = false>
-__global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
     __shared__ float4 s_tab[kTabN];
+    __shared__ double s_b64[96];  // second certificate tables (rare path)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kE16CPW;
     const int k = lane & 7, h = (lane >> 4) & 1;
@@ -745,7 +824,10 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
     const bool valid = g < P.n_cubes;
     uint2 raw[4];
     e16_load(P, g, valid, k, h, raw);
-    if (!MEM && blockIdx.x == 0 && threadIdx.x == 0 && P.replay_clear) *P.replay_clear = 0u;
+    if (!MEM && blockIdx.x == 0 && P.replay_clear) {
+#pragma unroll
+        for (int i = 0; i < 2 * kCountSpread / kBlock; i++) P.replay_clear[i * kBlock + threadIdx.x] = 0u;
+    }
     if (cube0 >= P.n_cubes) return;  // wave-uniform
     char* wl = lds + wave * kE16Lds;
     int32_t qv[8][4];
@@ -759,18 +841,19 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
         enc_tables(P, s_tab, lane);
         e16_body(P, raw, wl, s_tab, lane, valid, qv, fm);
     }
+    // ---- rare path, part 1: the second certificate's loads, issued before the stores (a load issued
+    //      after them would wait for them too: one in-order vmcnt) ----
+    const bool rare = !MEM && P.recheck && __builtin_expect(__ballot(fm != 0u) != 0ull, 0);  // wave-uniform
+    uint2 raw2[4];
+    double bv = 0.0, tv = 0.0;
+    if (rare) {
+        e16_load(P, g, valid, k, h, raw2);
+        bv = P.tab64[lane];
+        tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
+    }
 
-    // ---- rare path, part 1: the first uncertified coefficient's replay loads, issued before the
-    //      stores (a load issued after them would wait for them: one in-order vmcnt) ----
     const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
                        P.ngroups, P.coef, P.group_of};
-    const bool rare = !MEM && __ballot(fm != 0u) != 0ull;  // wave-uniform
-    ReplayIn rin;
-    uint32_t rg = 0, rk = 0;
-    if (__builtin_expect(rare, 0)) {
-        e16_flag_pos(fm, (int)__builtin_ctzll(__ballot(fm != 0u)), cube0, rg, rk);
-        rin = replay_load<8>(R, rg, rk, lane);
-    }
 
     // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
 #pragma unroll
@@ -796,27 +879,40 @@ __global__ __launch_bounds__(kBlock) void encode16_kernel(EncodeParams P) {
         wave_lds_sync();
     }
 
-    // ---- rare path, part 2: the exact Java fold of every uncertified coefficient (whole wave, one at
-    //      a time), written over the stored value by lane 0.  The wave's own earlier store of that word
-    //      is complete first (vmcnt(0)), so the exact value is the one that stays. ----
-    if (__builtin_expect(rare, 0)) {
+    // ---- rare path, part 2: the second certificate (one counter update per wave) ----
+    if (rare) {
+        uint32_t nset;
+        e16_recheck64(P, raw2, bv, tv, s_b64, lane, cube0, fm, nset);
+        for (int o = 1; o < 64; o <<= 1) nset += __shfl_xor(nset, o, 64);
+        if (lane == 0 && nset && P.replay_count)
+            atomicAdd(P.replay_count + kCountSpread + (blockIdx.x & (kCountSpread - 1)), nset);
+    }
+
+    // ---- rarest path: the exact Java fold of every coefficient both certificates left open (exact
+    //      ties, e.g. k = (0, 2, 2) where the basis products lie in Q(sqrt 2) and the value can be a
+    //      rational x.5 exactly: a few per 10^8 coefficients), whole wave, one at a time, written over
+    //      the stored value by lane 0.  Its loads wait for the wave's stores (one in-order vmcnt), and
+    //      lane 0's store follows its own earlier store of that word (vmcnt(0)), so the exact value is
+    //      the one that stays. ----
+    if (__builtin_expect(!MEM && __ballot(fm != 0u) != 0ull, 0)) {
         char* rs = wl;  // the wave's region is free again (its last staging round is stored)
         uint32_t n = 0;
         for (;;) {
-            const int q = replay_fold<8, true>(rin, rk, lane, (int*)rs, (double*)(rs + kMaxGroupsDev * 4));
+            const uint64_t who = __ballot(fm != 0u);
+            if (who == 0ull) break;
+            const int src = (int)__builtin_ctzll(who);
+            uint32_t rg, rk;
+            e16_flag_pos(fm, src, cube0, rg, rk);
+            const int q = replay_fold<8, true>(replay_load<8>(R, rg, rk, lane), rk, lane, (int*)rs,
+                                               (double*)(rs + kMaxGroupsDev * 4));
             if (lane == 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 P.out[(size_t)rg * CS + rk] = q;
             }
             n++;
-            const int src = (int)__builtin_ctzll(__ballot(fm != 0u));  // the coefficient just replayed
             if (lane == src) fm &= fm - 1u;
-            const uint64_t who = __ballot(fm != 0u);
-            if (who == 0ull) break;
-            e16_flag_pos(fm, (int)__builtin_ctzll(who), cube0, rg, rk);
-            rin = replay_load<8>(R, rg, rk, lane);
         }
-        if (lane == 0 && P.replay_count) atomicAdd(P.replay_count, n);
+        if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), n);
     }
 }
 

@@ -428,6 +428,55 @@ bool build_plan(int cw, int ch, int cd, Plan& p) {
         p.enc_E[s] = std::nextafter((float)(E[s] + 2e-7), INFINITY);
     }
 
+    // ---- second certificate (8x8x8): fp64 re-evaluation of a coefficient the fp32 one leaves open ----
+    // The kernel (e16_recheck64) computes v64 = sum over its 16 lanes of
+    //   b[ky][y] * sum_e b[kz][4h+e] * sum_x x * b[kx][x]     (fp64 fma chains, xor-butterfly sum)
+    // with b = basis64 (each entry the double nearest the exact basis value).  Against the exact
+    // value V = sum_n x_n c_n (c_n the exact orthonormal basis product, 0 <= x_n <= 255):
+    //   |v64 - V|    <= 72 u * 255 * L1x          (3 representation + 8 fma + 2 mul + 2 fma + 4 add
+    //                                              roundings, each <= u * sum |terms|; 72u leaves 3x)
+    //   |v_java - V| <= 255 * devx + (ng + 2) u * 255 * L1j
+    //        devx = sum_n |cj_n - c_n|, cj_n = Java's group coefficient of input n (0 if dropped:
+    //        DCT.java:84), L1j = sum_n |cj_n| (the fold's ng products and additions, DCT.java:49-52)
+    // Both quotients by the step round once more (|q| < 2^12: 2^-40 each).  So with
+    //   E64 = (255 devx + (ng + 2) u 255 L1j + 72 u 255 L1x) / step + 2^-38,
+    // |q64 - rint(q64)| < 0.5 - E64 implies Math.round(v_java / step) = rint(q64).  The table holds
+    // 0.5 - 2 max_k E64 per s (a further factor 2).  Exact values: long double (64-bit mantissa).
+    if (cd == 8) {
+        const long double pi = 3.141592653589793238462643383279502884L;
+        long double bl[8][8];
+        for (int kk = 0; kk < 8; kk++)
+            for (int n = 0; n < 8; n++) {
+                bl[kk][n] = (kk == 0 ? sqrtl(0.125L) : 0.5L) * cosl(pi * (long double)((2 * n + 1) * kk) / 16.0L);
+                p.basis64[kk * 8 + n] = (double)bl[kk][n];
+            }
+        const long double u = ldexpl(1.0L, -53);
+        long double E64[kMaxS] = {};
+        for (int kz = 0; kz < 8; kz++)
+            for (int ky = 0; ky < 8; ky++)
+                for (int kx = 0; kx < 8; kx++) {
+                    const int k = (kz * 8 + ky) * 8 + kx, s = kx + ky + kz;
+                    if (s == 0) continue;
+                    long double devx = 0, L1x = 0, L1j = 0;
+                    for (int z = 0; z < 8; z++)
+                        for (int y = 0; y < 8; y++)
+                            for (int x = 0; x < 8; x++) {
+                                const int n = (z * 8 + y) * 8 + x;
+                                const long double ex = bl[kz][z] * bl[ky][y] * bl[kx][x];
+                                const uint8_t go = p.fwd_group_of[(size_t)k * cs + n];
+                                const long double cj = go == 0xFF ? 0.0L : (long double)p.fwd_coef[(size_t)k * kMaxGroups + go];
+                                devx += fabsl(cj - ex);
+                                L1x += fabsl(ex);
+                                L1j += fabsl(cj);
+                            }
+                    const long double e = (255.0L * devx + (p.fwd_ngroups[k] + 2) * u * 255.0L * L1j +
+                                           72.0L * u * 255.0L * L1x) / (long double)(5 * s) +
+                                          ldexpl(1.0L, -38);
+                    E64[s] = std::max(E64[s], e);
+                }
+        for (int s = 0; s < kMaxS; s++) p.enc_thr64[s] = s == 0 ? 0.5 : (double)(0.5L - 2.0L * E64[s]);
+    }
+
     // ---- decoder certification (fp64 kernel vs the Java fold) ----
     std::vector<double> Kd, L1d;
     analyse_decoder(p, Kd, L1d);

@@ -34,6 +34,12 @@ struct Plan {
     std::vector<double> enc_L1;           // [cs] sum_n |basis|
     std::vector<double> enc_dev;          // [cs] grouping deviation bound (coef_g vs own coef)
 
+    // ---- second certificate (8x8x8 encode, rare path): a coefficient the fp32 certificate leaves
+    //      open is re-evaluated in fp64 as sum_n x_n * b[kz][z] b[ky][y] b[kx][x]; it is settled iff
+    //      |q64 - rint(q64)| < enc_thr64[s] (q64 = v64 / step), else it goes to the exact Java fold ----
+    double basis64[64] = {};              // orthonormal 8-point DCT-II basis [k][n], fp64
+    double enc_thr64[kMaxS] = {};         // 0.5 - 2 * max_k E64_k per s (bound derivation: dct3d_plan.cpp)
+
     // ---- fused-decode certification (fp64 kernel) ----
     // |v_fp64 - v_java| <= A_in * dec_G + dec_E, A_in = max |dequantised coefficient| in the cube.
     double dec_G = 0.0, dec_E = 0.0;

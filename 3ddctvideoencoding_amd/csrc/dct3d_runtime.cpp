@@ -61,14 +61,21 @@ struct dct3d_ctx {
     uint64_t n_timed = 0;
     double kernel_ms = 0.0, fixup_ms = 0.0;
     // plan tables on device
-    DevBuf d_ngroups, d_coef, d_group_of, d_inv_coef, d_tabs;
+    DevBuf d_ngroups, d_coef, d_group_of, d_inv_coef, d_tabs, d_tabs64;
+    // test / diagnostic options (dct3d_ctx_set_option): how later calls reach their results
+    uint32_t opt_flag_cap = 0;      // 0: default capacity
+    double opt_dec_margin = 0.0;    // added to the decode margin
+    bool opt_enc_no_recheck = false, opt_eg_single_pass = false, opt_eg_two_step = false,
+         opt_eg_no_resolve = false;
     // certify-or-replay state
     DevBuf d_flags, d_cubes, d_counters;
     uint32_t flag_cap = 0;
     uint64_t last_units = 0;
     bool last_valid = false;
     // in-wave replay (8x8x8 encode): two counter slots that alternate between calls; each launch zeroes
-    // the other slot for the next call, so a call needs no reset copy (zeroed once at creation)
+    // the other slot for the next call, so a call needs no reset copy (zeroed once at creation).
+    // Slot j (2 kCountSpread words at j * 2 kCountSpread): Java-fold replays, then second-certificate
+    // settlements, each spread over kCountSpread words (dct3d_kernels.h).
     DevBuf d_enc_counts;
     int enc_slot = 0;
     int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
@@ -153,6 +160,7 @@ int dct3d_plan_query(int bw, int bh, int bd, dct3d_plan_info* info, int32_t* ngr
         memcpy(info->enc_rstep, p.enc_rstep, sizeof(info->enc_rstep));
         memcpy(info->enc_G, p.enc_G, sizeof(info->enc_G));
         memcpy(info->enc_E, p.enc_E, sizeof(info->enc_E));
+        memcpy(info->enc_thr64, p.enc_thr64, sizeof(info->enc_thr64));
     }
     if (ngroups) memcpy(ngroups, p.fwd_ngroups.data(), sizeof(int32_t) * p.cs);
     if (coef) memcpy(coef, p.fwd_coef.data(), sizeof(double) * p.fwd_coef.size());
@@ -204,9 +212,15 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         rc = upload(c->d_inv_coef, t.data(), t.size() * sizeof(double));
     }
     if (!rc) rc = upload(c->d_tabs, tabs, sizeof(tabs));
+    if (!rc) {  // second certificate (8x8x8): [64] fp64 basis, [32] thresholds
+        double t64[64 + kMaxS];
+        memcpy(t64, p.basis64, sizeof(p.basis64));
+        memcpy(t64 + 64, p.enc_thr64, sizeof(p.enc_thr64));
+        rc = upload(c->d_tabs64, t64, sizeof(t64));
+    }
     if (!rc) rc = c->d_counters.grow(16);
-    if (!rc) rc = c->d_enc_counts.grow(16);
-    if (!rc && hipMemset(c->d_enc_counts.p, 0, 16) != hipSuccess) rc = DCT3D_EDEVICE;
+    if (!rc) rc = c->d_enc_counts.grow(4 * kCountSpread * sizeof(uint32_t));
+    if (!rc && hipMemset(c->d_enc_counts.p, 0, 4 * kCountSpread * sizeof(uint32_t)) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc) {
         std::vector<uint16_t> diag(p.cs);
         diagonal_order(block_w, block_h, block_d, diag.data());
@@ -226,7 +240,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_flags,
+    for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_tabs64, &c->d_flags,
                       &c->d_cubes, &c->d_counters, &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egf_slot,
@@ -249,6 +263,22 @@ int dct3d_ctx_set_stream(dct3d_ctx* c, void* s) {
     if (!c) return DCT3D_EINVAL;
     c->stream = s ? (hipStream_t)s : c->own_stream;
     return DCT3D_OK;
+}
+
+int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
+    if (!c || !(value >= 0.0)) return DCT3D_EINVAL;
+    switch (option) {
+        case DCT3D_OPT_FLAG_CAP:
+            if (value > 4294967295.0) return DCT3D_EINVAL;
+            c->opt_flag_cap = (uint32_t)value;
+            return DCT3D_OK;
+        case DCT3D_OPT_DEC_MARGIN: c->opt_dec_margin = value; return DCT3D_OK;
+        case DCT3D_OPT_ENC_NO_RECHECK: c->opt_enc_no_recheck = value != 0.0; return DCT3D_OK;
+        case DCT3D_OPT_EG_SINGLE_PASS: c->opt_eg_single_pass = value != 0.0; return DCT3D_OK;
+        case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
+        case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
+        default: return DCT3D_EINVAL;
+    }
 }
 
 int dct3d_ctx_set_profiling(dct3d_ctx* c, int on) {
@@ -311,9 +341,16 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
     if (!c->last_valid) return DCT3D_OK;
     uint32_t cnt[4] = {0, 0, 0, 0};
     if (c->last_count_slot >= 0) {  // in-wave replay: the call's slot; no overflow path exists
-        if (hipMemcpyAsync(cnt, (uint32_t*)c->d_enc_counts.p + c->last_count_slot, 4, hipMemcpyDeviceToHost,
-                           c->stream) != hipSuccess)
+        std::vector<uint32_t> w(2 * kCountSpread);
+        if (hipMemcpyAsync(w.data(), (uint32_t*)c->d_enc_counts.p + c->last_count_slot * 2 * kCountSpread,
+                           w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
             return DCT3D_EDEVICE;
+        for (int i = 0; i < kCountSpread; i++) {
+            st->n_flagged += w[i];
+            st->n_rechecked += w[kCountSpread + i];
+        }
+        return DCT3D_OK;
     } else if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
         return DCT3D_EDEVICE;
     }
@@ -339,11 +376,8 @@ static int ensure_flag_buffers(dct3d_ctx* c, uint64_t n_cubes) {
     // wrong results.  cube list: one entry per cube at most.
     uint64_t cap = n_cubes * (uint64_t)c->plan.cs / 64 + 4096;
     if (cap > 0xFFFFFFF0ull) cap = 0xFFFFFFF0ull;
-    // test knob: shrink the list to exercise the whole-cube replay path (tests/test_gpu_parity.py)
-    if (const char* e = getenv("DCT3D_FLAG_CAP")) {
-        unsigned long long v = strtoull(e, nullptr, 10);
-        if (v < cap) cap = v;
-    }
+    // test option: shrink the list to exercise the whole-cube replay path (tests/test_gpu_parity.py)
+    if (c->opt_flag_cap && c->opt_flag_cap < cap) cap = c->opt_flag_cap;
     int rc = c->d_flags.grow(cap * sizeof(unsigned long long));
     if (rc) return rc;
     rc = c->d_cubes.grow((n_cubes + 1) * sizeof(uint32_t));
@@ -409,8 +443,10 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.coef = (const double*)c->d_coef.p;
     P.group_of = (const uint8_t*)c->d_group_of.p;
     if (inwave) {
-        P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot;
-        P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1);
+        P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
+        P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+        P.tab64 = (const double*)c->d_tabs64.p;
+        P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
     }
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
@@ -499,9 +535,9 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     P.stack_stride = plane * D;
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
-    // test knob: widen the certification margin so that most pixels are uncertified and their cubes
+    // test option: widen the certification margin so that most pixels are uncertified and their cubes
     // take the whole-cube replay path (tests/test_gpu_parity.py); a wider margin is never unsafe
-    if (const char* e = getenv("DCT3D_DEC_MARGIN_BOOST")) P.dec_E += fabs(atof(e));
+    P.dec_E += c->opt_dec_margin;
     P.flag_list = (unsigned long long*)c->d_flags.p;
     P.counters = (unsigned int*)c->d_counters.p;
     P.flag_cap = c->flag_cap;
@@ -822,10 +858,9 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     // worst case per lane: cs/8 values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 14 bits)
     const uint32_t seg_cap = (uint32_t)(64 * (((c->plan.cs / 8) * 27 + 31) / 32));
     // two passes (the default): K1 codes into per-segment slots, then scan + compaction.  The single pass
-    // (DCT3D_EG_SINGLE_PASS=1: K1 places the stream itself after a decoupled look-back) writes the same
+    // (DCT3D_OPT_EG_SINGLE_PASS: K1 places the stream itself after a decoupled look-back) writes the same
     // stream but measured slower; a look-back that gives up falls back to two passes
-    const char* one = getenv("DCT3D_EG_SINGLE_PASS");
-    bool sp = one && *one && strcmp(one, "0");
+    bool sp = c->opt_eg_single_pass;
     if ((rc = sp ? c->d_egf_state.grow(n_seg * sizeof(uint64_t)) : 0) ||
         (rc = sp ? 0 : c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
         (rc = sp ? 0 : c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
@@ -927,10 +962,7 @@ int dct3d_encode_eg(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n_sta
         return rc;
     if (n_cubes && hipMemcpyAsync(c->h_in.p, raster, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
-    static const bool two_step = [] {  // A/B knob: encode to int32 cube-major, then the stand-alone EG stage
-        const char* e = getenv("DCT3D_EG_TWO_STEP");
-        return e && atoi(e) != 0;
-    }();
+    const bool two_step = c->opt_eg_two_step;  // A/B option: int32 cube-major, then the stand-alone EG stage
     if (!two_step) {
         uint64_t cap = in_bytes + 64, tb = 0;
         for (int attempt = 0; attempt < 2; attempt++) {
@@ -1005,9 +1037,8 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.q = nullptr;
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts and, resolving,
     // usually proves every chunk in sync by itself; otherwise confirming passes follow); at most
-    // n_chunks + 1 passes by induction from chunk 0.  DCT3D_EG_NO_RESOLVE: always confirm (A/B, tests)
-    const char* no_resolve = getenv("DCT3D_EG_NO_RESOLVE");
-    const bool resolve = !no_resolve || !*no_resolve || !strcmp(no_resolve, "0");
+    // n_chunks + 1 passes by induction from chunk 0.  DCT3D_OPT_EG_NO_RESOLVE: always confirm (A/B, tests)
+    const bool resolve = !c->opt_eg_no_resolve;
     int cur = 0;
     for (uint64_t it = 0; it <= n_chunks + 1; it++) {
         if (hipMemsetAsync(c->d_egd_status.p, 0, 32, c->stream) != hipSuccess) return DCT3D_EDEVICE;
@@ -1091,7 +1122,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     P.stack_stride = plane * D;
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
-    if (const char* e = getenv("DCT3D_DEC_MARGIN_BOOST")) P.dec_E += fabs(atof(e));  // test knob (see above)
+    P.dec_E += c->opt_dec_margin;  // test option (see above)
     P.flag_list = (unsigned long long*)c->d_flags.p;
     P.counters = (unsigned int*)c->d_counters.p;
     P.flag_cap = c->flag_cap;

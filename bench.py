@@ -506,6 +506,7 @@ def main():
         },
         "ceiling": ceiling,
         "flagged_units_last_step": st["n_flagged"],
+        "rechecked_units_last_step": st.get("n_rechecked", 0),
         "units_per_step": st["n_units"],
         "mcubes_per_s_per_gpu": value / world / 1e6,
         "eg_stage": None if direction not in ("encode_eg", "decode_eg") else {

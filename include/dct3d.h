@@ -60,7 +60,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written past its end) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 4
+#define DCT3D_ABI_VERSION 5
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -73,6 +73,8 @@ typedef struct {
     uint64_t n_timed;          /* calls timed */
     double kernel_ms_total;    /* main transform kernel, summed */
     double fixup_ms_total;     /* exact-fold kernel, summed */
+    uint64_t n_rechecked;      /* 8x8x8 encode: units of the last call the fp32 certificate left open
+                                  and the fp64 second certificate settled (not counted in n_flagged) */
 } dct3d_stats;
 
 /* Transform-plan introspection (host only, no device needed). */
@@ -85,6 +87,7 @@ typedef struct {
     float enc_rstep[32];  /* encode certification per s = kx+ky+kz: fp32(1/max(1,5s)) */
     float enc_G[32];      /*   threshold_s = 0.5 - (A * G_s + E_s), A = max|x - mean| of the cube */
     float enc_E[32];
+    double enc_thr64[32]; /* 8x8x8 second certificate: settled iff |q64 - rint(q64)| < enc_thr64[s] */
 } dct3d_plan_info;
 
 /* The plan for block dims (bw, bh, bd): the MI355X build's DCT.initialize (DCT.java:77-163) and
@@ -111,6 +114,18 @@ void dct3d_ctx_destroy(dct3d_ctx *ctx);
 /* Use an external hipStream_t (e.g. a framework's current stream) instead of the ctx-owned one.
  * NULL restores the ctx-owned stream. */
 int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
+/* Test / diagnostic options of a ctx.  Each one changes only HOW later calls reach their results
+ * (the results stay bit-identical): tests use them to drive the rare paths.  value 0 restores the
+ * default.  Unknown options: DCT3D_EINVAL. */
+#define DCT3D_OPT_FLAG_CAP 1          /* flag-list capacity in entries (8x8x4 encode, decode): overflow
+                                         sends cubes to the whole-cube replay */
+#define DCT3D_OPT_DEC_MARGIN 2        /* added to the decode certification margin: cubes go to the replay */
+#define DCT3D_OPT_ENC_NO_RECHECK 3    /* 1: the 8x8x8 encode skips its fp64 second certificate, so every
+                                         coefficient the fp32 certificate leaves open takes the Java fold */
+#define DCT3D_OPT_EG_SINGLE_PASS 4    /* 1: fused encode + Exp-Golomb by decoupled look-back (one pass) */
+#define DCT3D_OPT_EG_TWO_STEP 5       /* 1: dct3d_encode_eg / dct3d_decode_eg through int32 cubes */
+#define DCT3D_OPT_EG_NO_RESOLVE 6     /* 1: Exp-Golomb decode sync by plain confirming passes only */
+int dct3d_ctx_set_option(dct3d_ctx *ctx, int option, double value);
 /* Enable HIP-event timing of the kernels (reported by dct3d_get_stats). */
 int dct3d_ctx_set_profiling(dct3d_ctx *ctx, int on);
 int dct3d_synchronize(dct3d_ctx *ctx);

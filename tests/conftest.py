@@ -3,6 +3,7 @@
 `-m gpu` tests run on a real MI355X (they call the HIP library through its C-ABI and compare with
 the oracle); everything else is CPU-only (oracle vs golden fixtures, host codec, ABI exports).
 """
+import contextlib
 import importlib
 import os
 import sys
@@ -41,6 +42,16 @@ def plan8(oracle):
 @pytest.fixture(scope="session")
 def plan4(oracle):
     return oracle.Plan(8, 8, 4)
+
+
+@contextlib.contextmanager
+def ctx_option(ctx, option, value):
+    """Set a test / diagnostic option (DCT3D_OPT_*) on a context for the duration of a block."""
+    ctx.set_option(option, value)
+    try:
+        yield ctx
+    finally:
+        ctx.set_option(option, 0)
 
 
 @pytest.fixture(scope="session")

@@ -7,6 +7,8 @@ byte is carried, ExpGolomb.c:112-130).  Bit-exact comparisons only."""
 import numpy as np
 import pytest
 
+from conftest import ctx_option
+
 pytestmark = pytest.mark.gpu
 
 
@@ -183,21 +185,20 @@ def test_decode_eg_host_path_and_batches(pkg, oracle, plan8, plan4, depth):
 
 @pytest.mark.parametrize("confirm", [False, True])
 @pytest.mark.parametrize("big_frac", [0.0, 0.02])
-def test_eg_decode_resolve_and_confirming_passes(pkg, oracle, gpu_ctx8, monkeypatch, confirm, big_frac):
+def test_eg_decode_resolve_and_confirming_passes(pkg, oracle, gpu_ctx8, confirm, big_frac):
     """Pass 0 with the in-block resolve (each chunk's true parse walked beside its pass-0 parse until
     they meet) and the plain confirming passes (DCT3D_EG_NO_RESOLVE) give the same values.  With long
     codes (|v| up to 2^30: 61-bit codes) some chunks do not meet within the 128-bit walk: their inline
     re-parse runs, and where a chunk's true exit differs from its pass-0 exit the host's confirming
     passes follow."""
-    if confirm:
-        monkeypatch.setenv("DCT3D_EG_NO_RESOLVE", "1")
     rng = np.random.default_rng(99)
     q = rng.integers(-30, 31, size=(2500, 8, 8, 8)).astype(np.int32)
     q[rng.random(q.shape) < 0.6] = 0
     big = rng.random(q.shape) < big_frac
     q[big] = rng.integers(-(2**30) + 1, 2**30, size=int(big.sum()))
     data, nbits = _expected(oracle, pkg, q, 8)
-    got, eb = _eg_decode(gpu_ctx8, data, q.shape[0])
+    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_NO_RESOLVE, 1 if confirm else 0):
+        got, eb = _eg_decode(gpu_ctx8, data, q.shape[0])
     assert eb == nbits and np.array_equal(got, q)
 
 

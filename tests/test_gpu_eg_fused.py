@@ -9,6 +9,7 @@ against the oracle in test_gpu_parity.py / test_gpu_eg.py) at 1080p."""
 import numpy as np
 import pytest
 
+from conftest import ctx_option
 from test_gpu_eg import _expected, _gpu_stream
 
 pytestmark = pytest.mark.gpu
@@ -65,15 +66,15 @@ def test_fused_ragged_segment_tails(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("w,h,stacks", [(8, 8, 1), (40, 8, 5), (136, 72, 2)])
 @pytest.mark.parametrize("carry_bits", [0, 3])
-def test_fused_single_pass_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, monkeypatch, depth, w, h,
+def test_fused_single_pass_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, w, h,
                                           stacks, carry_bits):
-    """DCT3D_EG_SINGLE_PASS=1 on small and ragged inputs (one segment, a partial last segment, the
+    """DCT3D_OPT_EG_SINGLE_PASS on small and ragged inputs (one segment, a partial last segment, the
     carried byte taken by segment 0's look-back) against the oracle's stream"""
-    monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
     ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
     fr = pkg.synthetic.frames(w, h, stacks * depth, kind="uniform", frame0=w + carry_bits)
     exp, ebits = _expected(oracle, pkg, plan.encode_q(fr), depth, 0x3C, carry_bits)
-    got, tb, raw = _fused(ctx, fr, 0x3C, carry_bits)
+    with ctx_option(ctx, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1):
+        got, tb, raw = _fused(ctx, fr, 0x3C, carry_bits)
     assert tb == ebits and got == exp
     assert not raw[len(got):(tb + 31) // 32 * 4].any()
 
@@ -109,23 +110,26 @@ def test_fused_1080p_matches_oracle(pkg, oracle, plan8, gpu_ctx8):
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("kind", ["uniform", "checker"])
 @pytest.mark.parametrize("carry_bits", [0, 5])
-def test_fused_single_pass_matches_two_pass(pkg, gpu_ctx8, gpu_ctx4, monkeypatch, depth, kind, carry_bits):
-    """DCT3D_EG_SINGLE_PASS=1 (each wave places its bits after a decoupled look-back over the earlier
+def test_fused_single_pass_matches_two_pass(pkg, gpu_ctx8, gpu_ctx4, depth, kind, carry_bits):
+    """DCT3D_OPT_EG_SINGLE_PASS (each wave places its bits after a decoupled look-back over the earlier
     segments' totals) and the default two passes (slots + scan + compaction) write the same stream;
     1080p x 3 stacks is ~49k segments, so look-backs run across many waves still in flight"""
     ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
     fr = _content(pkg, kind, 1920, 1080, 3 * depth) if kind != "uniform" else \
         pkg.synthetic.frames(1920, 1080, 3 * depth, kind="uniform", frame0=11)
     tp, ttp, _ = _fused(ctx, fr, 0xA5, carry_bits)
-    monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
-    sp, tsp, _ = _fused(ctx, fr, 0xA5, carry_bits)
+    with ctx_option(ctx, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1):
+        sp, tsp, _ = _fused(ctx, fr, 0xA5, carry_bits)
     assert tsp == ttp and sp == tp
 
 
 @pytest.mark.parametrize("single_pass", [False, True])
-def test_fused_capacity(pkg, gpu_ctx8, monkeypatch, single_pass):
-    if single_pass:
-        monkeypatch.setenv("DCT3D_EG_SINGLE_PASS", "1")
+def test_fused_capacity(pkg, gpu_ctx8, single_pass):
+    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1 if single_pass else 0):
+        _fused_capacity(pkg, gpu_ctx8, single_pass)
+
+
+def _fused_capacity(pkg, gpu_ctx8, single_pass):
     fr = pkg.synthetic.frames(64, 64, 8, kind="uniform")
     _, tb, _ = _fused(gpu_ctx8, fr)
     import torch
@@ -219,14 +223,14 @@ def test_fused_decode_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ct
     assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
 
 
-def test_fused_decode_whole_cube_replay_from_stream(pkg, gpu_ctx8, monkeypatch):
+def test_fused_decode_whole_cube_replay_from_stream(pkg, gpu_ctx8):
     """a widened certification margin sends cubes to the replay, which re-parses them from the stream"""
     fr = pkg.synthetic.frames(256, 128, 16, kind="uniform", frame0=9)
     data, _ = gpu_ctx8.encode_eg(fr)
     ref, _ = _decode_two_step(gpu_ctx8, data, 256, 128, 2)
-    monkeypatch.setenv("DCT3D_DEC_MARGIN_BOOST", "0.45")
-    got, _ = _decode_fused(gpu_ctx8, data, 256, 128, 2)
-    assert gpu_ctx8.stats()["n_overflow_cubes"] > 0       # the replay path ran
+    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_DEC_MARGIN, 0.45):
+        got, _ = _decode_fused(gpu_ctx8, data, 256, 128, 2)
+        assert gpu_ctx8.stats()["n_overflow_cubes"] > 0   # the replay path ran
     assert np.array_equal(got, ref)
 
 

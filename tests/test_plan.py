@@ -42,3 +42,114 @@ def test_invalid_block_dims(pkg):
         pkg.plan_query(8, 8, 5)
     with pytest.raises(pkg.Dct3dError):
         pkg.plan_query(4, 4, 4)
+
+
+def test_second_certificate_bound(pkg, oracle, plan8):
+    """The 8x8x8 second certificate (e16_recheck64): an fp64 evaluation v64 of every coefficient from
+    the cube's bytes and the fp64 basis lies within E64 = (0.5 - thr64[s]) / 2 of Java's fold value
+    (DCT.java:44-52, the oracle) in units of the step, on uniform noise and extreme patterns -- and so
+    every coefficient it settles (|q64 - rint(q64)| < thr64) rounds to Java's Math.round.  numpy's
+    evaluation order differs from the kernel's; the bound (dct3d_plan.cpp) covers any order with at
+    most ~24 roundings per term, and the observed error is checked against it with room to spare."""
+    p = pkg.plan_query(8, 8, 8)
+    thr = p["enc_thr64"]
+    assert thr[0] == 0.5
+    e64 = (0.5 - thr[1:22]) / 2
+    assert (e64 > 0).all() and (e64 < 1e-9).all()
+    B = np.array([[(np.sqrt(0.125) if k == 0 else 0.5) * np.cos(np.pi * (2 * n + 1) * k / 16) for n in range(8)]
+                  for k in range(8)])
+    rng = np.random.default_rng(5)
+    z, y, x = np.meshgrid(np.arange(16), np.arange(64), np.arange(64), indexing="ij")
+    contents = [rng.integers(0, 256, size=(16, 64, 64)).astype(np.uint8),
+                (((x + y + z) % 2) * 255).astype(np.uint8), np.where(z % 8 < 4, 0, 255).astype(np.uint8)]
+    s = (np.arange(8)[:, None, None] + np.arange(8)[None, :, None] + np.arange(8)[None, None, :])
+    step = np.maximum(1, 5 * s)
+    worst = 0.0
+    for fr in contents:
+        q, d = plan8.encode_q(fr, want_dct=True)
+        cubes = oracle.to_cubes(fr).astype(np.float64)             # [n, z, y, x]
+        v64 = np.einsum("nzyx,cz,by,ax->ncba", cubes, B, B, B)     # [n, kz, ky, kx]
+        java = oracle.to_cubes(d)                                  # Java's fp64 DCT values, cube-major
+        err = np.abs(v64 - java) / step
+        bound = np.where(s == 0, np.inf, np.concatenate([[np.inf], e64, [np.inf] * 10])[s])
+        assert (err <= bound).all()
+        worst = max(worst, float((err / bound)[:, s > 0].max()))
+        q64 = v64 / step
+        settled = (np.abs(q64 - np.rint(q64)) < thr[s]) & (s > 0)
+        assert np.array_equal(np.rint(q64)[settled].astype(np.int32), q[settled])
+    assert worst < 0.25  # observed ~0.05
+
+
+def _java_hashmap_fold_order(cw, ch, cd, k0, k1, k2):
+    """Closed-form Java 8 HashMap<Long, Multiplication> iteration order for output coefficient
+    (k0, k1, k2) of DCT.initialize (DCT.java:93-133), written independently of the planner's
+    insert/resize emulation (csrc/dct3d_plan.cpp JavaLongMap) and of the oracle's:
+      * the coefficient expression, left to right as javac evaluates it (DCT.java:119), with the
+        Transform.java:20-21 constants; the key (long)(c * 1E9), zero keys dropped (DCT.java:122-123);
+      * HashMap iteration = bins in index order, each bin's list in insertion order (a resize splits
+        a bin into lo/hi lists that keep their relative order, so this holds at the final capacity);
+        bin = spread(Long.hashCode(key)) & (cap - 1), spread(h) = h ^ (h >>> 16);
+      * final capacity: 16 doubled while size > 0.75 cap (putVal's threshold), valid only if no bin
+        ever holds more than TREEIFY_THRESHOLD = 8 nodes (a 9th would resize below 64 or treeify),
+        checked for the keys each capacity holds (the first 0.75 cap + 1 inserted).
+    Returns the group coefficients in fold order and the fold index of every input n (-1: dropped)."""
+    import math
+    dim = math.sqrt(math.pow(2.0, 3.0))
+    inv_sqrt2 = 1.0 / math.sqrt(2.0)
+    f32 = lambda v: float(np.float32(v))
+    scale = dim / math.sqrt(cw * ch * cd)
+    pw, ph, pd = math.pi / f32(cw), math.pi / f32(ch), math.pi / f32(cd)
+    c0 = inv_sqrt2 if k0 == 0 else 1.0
+    c1 = inv_sqrt2 if k1 == 0 else 1.0
+    c2 = inv_sqrt2 if k2 == 0 else 1.0
+    first = {}          # key -> (insertion rank, coefficient)
+    key_of = []
+    for n0 in range(cd):
+        for n1 in range(ch):
+            for n2 in range(cw):
+                c = scale * c0 * c1 * c2 * math.cos(pd * f32(n0 + 0.5) * k0) * math.cos(ph * f32(n1 + 0.5) * k1) \
+                    * math.cos(pw * f32(n2 + 0.5) * k2)
+                key = int(c * 1e9)                       # (long) truncates toward zero
+                key_of.append(key)
+                if key != 0 and key not in first:
+                    first[key] = (len(first), c)
+
+    def bin_of(key, cap):
+        v = key & 0xFFFFFFFFFFFFFFFF
+        h = (v ^ (v >> 32)) & 0xFFFFFFFF                 # Long.hashCode
+        return (h ^ (h >> 16)) & (cap - 1)               # HashMap.hash, then index
+
+    cap = 16
+    while len(first) > 0.75 * cap:
+        cap *= 2
+    keys = sorted(first, key=lambda kk: first[kk][0])   # insertion order
+    c_ = 16
+    while c_ <= cap:                                     # no bin of 9 at any capacity on the way
+        held = keys[: int(0.75 * c_) + 1]
+        counts = np.bincount([bin_of(kk, c_) for kk in held], minlength=c_)
+        assert counts.max() <= 8, (k0, k1, k2, c_)
+        c_ *= 2
+    order = sorted(first, key=lambda kk: (bin_of(kk, cap), first[kk][0]))
+    pos = {kk: i for i, kk in enumerate(order)}
+    coefs = np.array([first[kk][1] for kk in order])
+    gof = np.array([pos[kk] if kk != 0 else -1 for kk in key_of])
+    return coefs, gof
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_hashmap_fold_order_closed_form(pkg, plan8, plan4, depth):
+    """the Java fold order decides the quantised value at exact ties (8x8x4: the
+    4-point k = 2 row is +-1/2; 8x8x8: e.g. k = (0, 2, 2), tests/test_gpu_parity.py).  The closed form
+    above must give, for every output coefficient, the same group coefficients in the same order and
+    the same membership as the product's planner (dct3d_plan_query) and the oracle."""
+    p = pkg.plan_query(8, 8, depth)
+    oplan = plan8 if depth == 8 else plan4
+    cs = 64 * depth
+    for k in range(cs):
+        k0, k1, k2 = k // 64, (k // 8) % 8, k % 8
+        coefs, gof = _java_hashmap_fold_order(8, 8, depth, k0, k1, k2)
+        ng = len(coefs)
+        assert p["ngroups"][k] == ng, k
+        assert np.array_equal(p["coef"][k, :ng], coefs), k          # bit-identical, same order
+        assert np.array_equal(np.where(p["group_of"][k] == 0xFF, -1, p["group_of"][k].astype(np.int64)), gof), k
+        assert np.array_equal(np.array([c for c, _ in oplan.groups(k)]), coefs), k
