@@ -1363,6 +1363,19 @@ __device__ __forceinline__ uint32_t cvt_u32_sat(double v) {
     return t;
 }
 
+// Fixed-point view of a decoded value, for the decode's certificate (decode_tile): with |v| < 2^19,
+// w = v + 1.5 * 2^20 lies in [2^20, 2^21), whose ulp is 2^-32, so one fp64 add (rounding error
+// <= 2^-33) leaves frac(v) * 2^32 in w's low word and 0x41380000 + floor(v) in its high word
+// (0x413: the biased exponent of 2^20; 2^19: the offset 0.5 * 2^20).
+constexpr double kFixMagic = 1572864.0;  // 1.5 * 2^20
+constexpr uint32_t kFixHi = 0x41380000u;
+// max(0, hi - kFixHi): max(0, floor(v)) in one VALU op (unsigned subtract, clamped at 0)
+__device__ __forceinline__ uint32_t fix_floor0(uint32_t hi) {
+    uint32_t t;
+    asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(hi), "s"(kFixHi));
+    return t;
+}
+
 // staged input of one tile (CPW cubes, 8 KiB): 8 coalesced 1 KiB loads per wave
 // (4-byte values: int32 quantised cubes, or the float cubes of the drop-in kernels)
 template <int D>
@@ -1587,10 +1600,18 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     }
 
     // ---- certify, clamp + truncate, store ----
-    const double m = amax * P.dec_G + P.dec_E + 0x1p-43;
+    // |v - v_java| <= m (dct3d_plan.cpp).  The byte is min(max(0, floor(v)), 255), monotone in v, so it
+    // is Java's byte when floor is constant over [v - m, v + m]: frac(v) >= m and frac(v) + m < 1.  In
+    // the fixed-point view (kFixMagic) lo = frac(v) 2^32 to within 1/2 unit, so with
+    // mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] proves it: (lo - mi) <= 2^32 - 1 - 2 mi
+    // as unsigned.  |v| < 2^19 holds when amax < 2^14: |v| <= amax * sum_k |c(n, k)| <= amax 8^1.5;
+    // a larger amax (never from an encoder of 8-bit frames) sends the cube to the replay.
+    const double m = amax * P.dec_G + P.dec_E;
+    const uint32_t mi = (uint32_t)__builtin_ceil(__fma_rn(m, 0x1p32, 0.5)) + 1u;  // + 1: m's own rounding
+    const uint32_t cert_lim = 0xFFFFFFFFu - 2u * mi;
     const int y = (D == 8) ? k : (4 * h + k);
     const int x0 = (D == 8) ? 4 * h : 0;
-    bool flag = q_range_bad;
+    bool flag = q_range_bad | (amax_f >= 16384.0f);
     uint32_t outw[D][NXC / 4];
     const uint32_t c255 = 255u;
 #pragma unroll
@@ -1600,9 +1621,9 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             uint32_t w = 0;
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                const double v = cz[z][4 * wd + e];
-                const uint32_t tl = cvt_u32_sat(v - m), th = cvt_u32_sat(v + m);
-                flag |= tl != th;
+                const uint64_t fx = __builtin_bit_cast(uint64_t, __dadd_rn(cz[z][4 * wd + e], kFixMagic));
+                const uint32_t tl = fix_floor0((uint32_t)(fx >> 32));
+                flag |= ((uint32_t)fx - mi) > cert_lim;
                 // byte e of w = min(tl, 255) (SDWA byte insert: the other bytes are preserved)
                 if (e == 0) w = min(tl, 255u);
                 else if (e == 1) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));

@@ -85,3 +85,42 @@ def test_bound_dominates_observed_error(emu, pkg, oracle, plan8, plan4, depth):
         assert (err <= bound).all()
         worst = max(worst, float((err / bound).max()))
     assert worst < 1.0
+
+
+def test_decode_fixed_point_certificate():
+    """decode_tile's certificate (dct3d_kernels.hip, kFixMagic): w = v + 1.5 * 2^20 in fp64, then
+    byte = min(max(0, hi(w) - 0x41380000), 255) and 'certified' iff (lo(w) - mi) <= 2^32 - 1 - 2 mi
+    (unsigned), mi = ceil(m 2^32 + 1/2) + 1.  Claim: when certified, every real value in [v - m, v + m]
+    maps to that byte under Java's (byte) clamp(x, 0, 255) of InverseDCT.java:74-80 (floor of the
+    clamped value).  Checked exactly (fractions) on random values, values within a few ulps of integers
+    and of the clamp ends, and several margins m."""
+    from fractions import Fraction
+    import math
+    rng = np.random.default_rng(17)
+    base = np.concatenate([rng.uniform(-600, 900, 4000), np.round(rng.uniform(-300, 560, 3000))])
+    vals = [float(v) for v in base]
+    for v in list(vals[4000:]):
+        vals += [math.nextafter(v, math.inf), math.nextafter(v, -math.inf), v + 2.0 ** -30, v - 2.0 ** -30,
+                 v + 3e-9, v - 3e-9]
+    vals += [0.0, -0.0, 255.0, 256.0, -1e-12, 255.999999999, 254.9999999999]
+
+    def java_byte(x):
+        x = min(max(x, Fraction(0)), Fraction(255))
+        return math.floor(x)
+
+    n_cert = n_flag = 0
+    for m in (1e-12, 6.6e-9, 1e-6):
+        mi = math.ceil(Fraction(m) * 2 ** 32 + Fraction(1, 2)) + 1
+        lim = 0xFFFFFFFF - 2 * mi
+        for v in vals:
+            w = np.float64(v) + np.float64(1572864.0)
+            bits = int(np.array([w]).view(np.uint64)[0])
+            hi, lo = bits >> 32, bits & 0xFFFFFFFF
+            byte = min(max(0, hi - 0x41380000), 255)
+            if ((lo - mi) & 0xFFFFFFFF) <= lim:
+                n_cert += 1
+                fv, fm = Fraction(v), Fraction(m)
+                assert java_byte(fv - fm) == byte == java_byte(fv + fm), (v, m)
+            else:
+                n_flag += 1
+    assert n_cert > 0 and n_flag > 0  # both outcomes exercised (most test values sit near integers)
