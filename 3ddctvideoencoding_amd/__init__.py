@@ -21,6 +21,7 @@ from . import synthetic  # noqa: F401  (integer-only generator shared with the d
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libdct3d.so")
+DIAG_LIB_PATH = os.path.join(LIB_DIR, "libdct3d_diag.so")  # measurement / test support (include/dct3d_diag.h)
 CODEC_LIB_PATH = os.path.join(LIB_DIR, "libdct3dcodec.so")
 CLI_PATH = os.path.join(LIB_DIR, "dct3d_codec")
 REPO_DIR = os.path.dirname(PKG_DIR)
@@ -28,20 +29,22 @@ INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
 DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
 # test / diagnostic options (include/dct3d.h, Context.set_option)
-(DCT3D_OPT_FLAG_CAP, DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_SINGLE_PASS, DCT3D_OPT_EG_TWO_STEP,
- DCT3D_OPT_EG_NO_RESOLVE) = 1, 2, 3, 4, 5, 6
+DCT3D_OPT_FLAG_CAP, DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 1, 2, 3, 5, 6
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
     "dct3d_abi_version", "dct3d_strerror", "dct3d_ctx_create", "dct3d_ctx_destroy",
-    "dct3d_ctx_set_stream", "dct3d_ctx_set_option", "dct3d_ctx_set_profiling", "dct3d_synchronize", "dct3d_get_stats",
+    "dct3d_ctx_set_stream", "dct3d_ctx_info", "dct3d_ctx_set_option", "dct3d_ctx_set_profiling", "dct3d_synchronize", "dct3d_get_stats",
     "dct3d_reset_timers",
     "dct3d_encode_stacks", "dct3d_encode_stacks_dev", "dct3d_decode_stacks", "dct3d_decode_stacks_dev",
     "dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev",
-    "dct3d_fill_synthetic_dev", "dct3d_plan_query", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
+    "dct3d_plan_query",
     "dct3d_eg_encode_dev", "dct3d_encode_eg", "dct3d_eg_fetch", "dct3d_diagonal_order",
     "dct3d_eg_decode_dev", "dct3d_decode_eg", "dct3d_encode_eg_dev", "dct3d_decode_eg_dev",
 )
+# Every symbol include/dct3d_diag.h declares (libdct3d_diag.so; none of them is in libdct3d.so).
+DIAG_SYMBOLS = ("dct3d_fill_synthetic_dev", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
+                "dct3d_decode_diag_dev")
 
 
 class Dct3dError(RuntimeError):
@@ -101,9 +104,7 @@ def lib() -> C.CDLL:
             getattr(L, name).argtypes = [vp, vp, i32, i32, i32, vp]
         for name in ("dct3d_forward_f32", "dct3d_inverse_f32", "dct3d_forward_f32_dev", "dct3d_inverse_f32_dev"):
             getattr(L, name).argtypes = [vp, vp, sz, vp]
-        L.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
-        L.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
-        L.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
+        L.dct3d_ctx_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(vp)]
         L.dct3d_plan_query.argtypes = [i32, i32, i32, C.POINTER(PlanInfo), vp, vp, vp, vp]
         L.dct3d_eg_encode_dev.argtypes = [vp, vp, u64, C.c_uint8, i32, vp, u64, C.POINTER(u64)]
         L.dct3d_encode_eg.argtypes = [vp, vp, i32, i32, i32, C.c_uint8, i32, C.POINTER(u64)]
@@ -115,6 +116,26 @@ def lib() -> C.CDLL:
         L.dct3d_decode_eg_dev.argtypes = [vp, vp, u64, u64, i32, i32, i32, vp, C.POINTER(u64)]
         _lib = L
     return _lib
+
+
+_diag = None
+
+
+def diag_lib() -> C.CDLL:
+    """Load libdct3d_diag.so (bench / test support: synthetic frames, memory-only twins, probes)."""
+    global _diag
+    if _diag is None:
+        lib()  # the product library first (the diag library links against it)
+        if not os.path.exists(DIAG_LIB_PATH):
+            raise ImportError(f"{DIAG_LIB_PATH} is missing: build it with `make`")
+        D = C.CDLL(DIAG_LIB_PATH)
+        vp, i32, sz, u64, i64 = C.c_void_p, C.c_int, C.c_size_t, C.c_uint64, C.c_int64
+        D.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
+        D.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
+        D.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
+        D.dct3d_decode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
+        _diag = D
+    return _diag
 
 
 def strerror(code: int) -> str:
@@ -283,14 +304,19 @@ class Context:
         _check(lib().dct3d_inverse_f32_dev(self._h, _tptr(d_in), n_cubes, _tptr(d_out)), "dct3d_inverse_f32_dev")
 
     def bandwidth_probe_dev(self, d_in, d_out, n_px: int, mode: int = 0) -> None:
-        _check(lib().dct3d_bandwidth_probe_dev(self._h, _tptr(d_in) if d_in is not None else None,
+        _check(diag_lib().dct3d_bandwidth_probe_dev(self._h, _tptr(d_in) if d_in is not None else None,
                                                _tptr(d_out) if d_out is not None else None, n_px, mode),
                "dct3d_bandwidth_probe_dev")
 
     def encode_memonly_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q) -> None:
         """Diagnostic: the encode's memory traffic without its compute (d_q is NOT a DCT)."""
-        _check(lib().dct3d_encode_memonly_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q)),
+        _check(diag_lib().dct3d_encode_memonly_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q)),
                "dct3d_encode_memonly_dev")
+
+    def decode_diag_dev(self, d_q, width: int, height: int, n_stacks: int, d_frames, mode: int) -> None:
+        """Diagnostic: the 8x8x8 decode's memory part (mode 1) or compute part (mode 2) alone."""
+        _check(diag_lib().dct3d_decode_diag_dev(self._h, _tptr(d_q), width, height, n_stacks, _tptr(d_frames), mode),
+               "dct3d_decode_diag_dev")
 
     # ---- Exp-Golomb stage (SURVEY.md §8f #1) ----
     def eg_encode_dev(self, d_q, n_cubes: int, d_out, out_cap: int, carry_byte: int = 0, carry_bits: int = 0) -> int:
@@ -355,5 +381,5 @@ class Context:
     def fill_synthetic_dev(self, d_frames, width: int, height: int, n_frames: int,
                            seed: int = synthetic.DEFAULT_SEED, frame0: int = 0, kind: str = "ramp") -> None:
         k = {"ramp": 0, "uniform": 1}[kind]
-        _check(lib().dct3d_fill_synthetic_dev(self._h, _tptr(d_frames), width, height, n_frames, seed, frame0, k),
+        _check(diag_lib().dct3d_fill_synthetic_dev(self._h, _tptr(d_frames), width, height, n_frames, seed, frame0, k),
                "dct3d_fill_synthetic_dev")

@@ -1,0 +1,369 @@
+// dct3d_decode_dev.h -- the decode kernel's device code (templates): staged loads -> dequantise ->
+// inverse passes -> certify -> raster stores.  Instantiated by dct3d_kernels.hip (the product) and
+// dct3d_diag.hip (the memory-only / compute-only split).
+#pragma once
+#include "dct3d_dev.h"
+
+namespace dct3d {
+
+// =============================================================================================
+// Fused decode (fp64, certified)
+// =============================================================================================
+// ---------------------------------------------------------------------------------------------
+// Decode v1: 2*D lanes per cube, 32 doubles per lane (<= 128 VGPRs, 4 waves per SIMD).
+//   lane = c2*32 + h*16 + c1*D + k   (cube c = c2*(CPW/2) + c1; h = bit 4; k = low bits)
+//   layout A (pass Y): lane (c, kz=k, h) holds b[ky][e], kx = 4h + e        (lines along ky)
+//   layout B (pass X): lane (c, kz=k, h) holds a[r][x],  y  = 4h + r        (lines along kx)
+//   layout C (pass Z): D=8: lane (c, y=k, h) holds cz[z][e], x = 4h + e      (lines along z)
+//                      D=4: lane (c, y=4h+k)  holds cz[z][x]
+//   A -> B is a lane-pair exchange (lanes l, l^16) by v_permlane16_swap: no LDS.
+//   B -> C goes through the wave's LDS region in two rounds (D=8: z halves, D=4: x halves), 8 KiB each.
+// Inputs are staged through the same region (1 KiB per load instruction).  The per-axis operation
+// sequence (dequantise, idct8/4 along Y, X, Z) is the one the planner's fp64 analysis bounds.
+// Certify + clamp: with m = amax*G + E (+2^-43 for the two roundings below, |v| < 1024),
+//   lo = v - m, hi = v + m;  out = min(cvt_u32(lo), 255)  unless cvt_u32(lo) != cvt_u32(hi).
+// cvt_u32 (v_cvt_u32_f64) truncates and saturates (negative -> 0), so min(cvt_u32(x), 255) is the
+// monotone map x -> (byte) clamp(x, 0, 255) of InverseDCT.java:74-80 / Decoder.java:112, and equal
+// values at lo and hi prove the Java value (within [lo, hi]) maps to the same byte.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDecWaveLds = 9216;
+
+template <int D>
+struct DecGeom {
+    static constexpr int CS = 64 * D;
+    static constexpr int LPC = 2 * D;          // lanes per cube
+    static constexpr int CPW = 64 / LPC;       // cubes per wave: 4 (D=8) | 8 (D=4)
+    static constexpr int SA_F = 288;           // staging face stride (256 B + 32 B pad)
+    static constexpr int SA_C = D * SA_F;      // staging cube stride
+    // B->C round strides (bank-conflict-free for D=8 by the guide's lane-group rules; D=4 best found)
+    static constexpr int TZ = (D == 8) ? 528 : 256;    // z stride (D=8: 8 rows x 64 B + 16)
+    static constexpr int TC = (D == 8) ? 2128 : 1040;  // cube stride
+    static_assert(CPW * SA_C <= kDecWaveLds && CPW * TC <= kDecWaveLds, "wave LDS region");
+    // slot of row y in face z (D=4 swizzles rows by z: bank spread of the 8-lane-per-cube reads)
+    static __device__ __forceinline__ int tslot(int z, int y) { return (D == 8) ? y : (y ^ z); }
+};
+
+__device__ __forceinline__ void swap16(double& a, double& b) {
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)ua, (uint32_t)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(ua >> 32), (uint32_t)(ub >> 32), false, false);
+    a = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    b = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+}
+
+__device__ __forceinline__ uint32_t cvt_u32_sat(double v) {
+    uint32_t t;
+    asm("v_cvt_u32_f64 %0, %1" : "=v"(t) : "v"(v));
+    return t;
+}
+
+// Fixed-point view of a decoded value, for the decode's certificate (decode_tile): with |v| < 2^19,
+// w = v + 1.5 * 2^20 lies in [2^20, 2^21), whose ulp is 2^-32, so one fp64 add (rounding error
+// <= 2^-33) leaves frac(v) * 2^32 in w's low word and 0x41380000 + floor(v) in its high word
+// (0x413: the biased exponent of 2^20; 2^19: the offset 0.5 * 2^20).
+constexpr double kFixMagic = 1572864.0;  // 1.5 * 2^20
+constexpr uint32_t kFixHi = 0x41380000u;
+// max(0, hi - kFixHi): max(0, floor(v)) in one VALU op (unsigned subtract, clamped at 0)
+__device__ __forceinline__ uint32_t fix_floor0(uint32_t hi) {
+    uint32_t t;
+    asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(hi), "s"(kFixHi));
+    return t;
+}
+
+// staged input of one tile (CPW cubes, 8 KiB): 8 coalesced 1 KiB loads per wave
+// (4-byte values: int32 quantised cubes, or the float cubes of the drop-in kernels)
+template <int D>
+__device__ __forceinline__ void dec_load_tile_p(const char* in, uint32_t n_cubes, uint32_t cube0, int lane,
+                                                int4 (&v)[8]) {
+    using G = DecGeom<D>;
+    const char* inb = in + (size_t)cube0 * G::CS * 4;
+    if (cube0 + G::CPW <= n_cubes) {  // wave-uniform: every cube of the tile exists
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const i32x4_t x = __builtin_nontemporal_load((const i32x4_t*)(inb + (size_t)(t * 64 + lane) * 16));
+            v[t] = make_int4(x.x, x.y, x.z, x.w);
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            const int q = t * 64 + lane;
+            v[t] = make_int4(0, 0, 0, 0);
+            if (cube0 + q / (G::CS / 4) < n_cubes) v[t] = *(const int4*)(inb + (size_t)q * 16);
+        }
+    }
+}
+template <int D>
+__device__ __forceinline__ void dec_load_tile(const DecodeParams& P, uint32_t cube0, int lane, int4 (&v)[8]) {
+    dec_load_tile_p<D>((const char*)P.in, P.n_cubes, cube0, lane, v);
+}
+template <int D>
+__device__ __forceinline__ void dec_stage_tile(char* wl, int lane, const int4 (&v)[8]) {
+    using G = DecGeom<D>;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const int q = t * 64 + lane;
+        *(int4*)(wl + (q / (G::CS / 4)) * G::SA_C + ((q >> 4) % D) * G::SA_F + (q & 15) * 16) = v[t];
+    }
+}
+
+// ---- B -> C through LDS in two rounds (D=8: z halves, D=4: x halves); every lane reads in
+//      every round into fixed registers (no lane-divergent definitions to merge) ----
+//   in:  layout B, lane (c, kz=k, h): row r (y = 4h + r): x 0..3 in b[r][.], x 4..7 in b[4 + r][.]
+//   out: layout C, D=8: lane (c, y=k, h) cz[z][e] (x = 4h + e); D=4: lane (c, y=4h+k) cz[z][x]
+template <int D>
+__device__ __forceinline__ void dec_b_to_c(const double (&b)[8][4], double (&cz)[D][(D == 8) ? 4 : 8], char* wl,
+                                           int c, int k, int h) {
+    using G = DecGeom<D>;
+#pragma unroll
+    for (int rd = 0; rd < 2; rd++) {
+        wave_lds_sync();
+        if constexpr (D == 8) {
+            if ((k >> 2) == rd) {  // writers: this round's z half; rows of 8 x (64 B)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    char* dst = wl + c * G::TC + (k & 3) * G::TZ + (4 * h + r) * 64;
+                    *(double2*)(dst) = make_double2(b[r][0], b[r][1]);
+                    *(double2*)(dst + 16) = make_double2(b[r][2], b[r][3]);
+                    *(double2*)(dst + 32) = make_double2(b[4 + r][0], b[4 + r][1]);
+                    *(double2*)(dst + 48) = make_double2(b[4 + r][2], b[4 + r][3]);
+                }
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int zr = 0; zr < 4; zr++) {
+                const char* src = wl + c * G::TC + zr * G::TZ + k * 64 + h * 32;
+                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
+                cz[4 * rd + zr][0] = t0.x; cz[4 * rd + zr][1] = t0.y;
+                cz[4 * rd + zr][2] = t1.x; cz[4 * rd + zr][3] = t1.y;
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const double* sv = (rd == 0) ? b[r] : b[4 + r];
+                char* dst = wl + c * G::TC + k * G::TZ + G::tslot(k, 4 * h + r) * 32;
+                *(double2*)(dst) = make_double2(sv[0], sv[1]);
+                *(double2*)(dst + 16) = make_double2(sv[2], sv[3]);
+            }
+            wave_lds_sync();
+            const int y = 4 * h + k;
+#pragma unroll
+            for (int z = 0; z < 4; z++) {
+                const char* src = wl + c * G::TC + z * G::TZ + G::tslot(z, y) * 32;
+                const double2 t0 = *(const double2*)(src), t1 = *(const double2*)(src + 16);
+                cz[z][4 * rd + 0] = t0.x; cz[z][4 * rd + 1] = t0.y;
+                cz[z][4 * rd + 2] = t1.x; cz[z][4 * rd + 3] = t1.y;
+            }
+        }
+    }
+}
+
+// One tile (CPW cubes) from the staged input in the wave's LDS region to the raster.  after_a() runs
+// once the staged input is in registers (the persistent variant issues the next tile's loads there).
+// PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
+template <int D, int PG, class AfterA>
+__device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
+                                            AfterA&& after_a) {
+    using G = DecGeom<D>;
+    constexpr int CPW = G::CPW;
+    constexpr int NXC = (D == 8) ? 4 : 8;  // x values per lane in layout C
+    const int h = (lane >> 4) & 1;
+    const int k = lane & (D - 1);
+    const int c = (lane >> 5) * (CPW / 2) + ((lane & 15) / D);
+    const uint32_t g = cube0 + c;
+    const bool valid = g < P.n_cubes;
+
+    // ---- layout A: dequantise, amax ----
+    // cf = q * step exactly: a 24-bit integer multiply (|q| < 2^23 checked; |q * step| < 2^30), then
+    // an exact conversion to fp64.  Out-of-range q (never produced by the encoder) sends the cube to
+    // the exact replay.  amax = max |q * step| from integer max / min.
+    double b[8][4];
+    float amax_f;
+    bool q_range_bad;
+    {
+        const int sb = 5 * (4 * h + k);                     // step = sb + 5 (e + ky); DC (e = ky = 0): 1
+        int stp[11];
+        stp[0] = max(sb, 1);
+#pragma unroll
+        for (int j = 1; j < 11; j++) stp[j] = sb + 5 * j;
+        const char* src = wl + c * G::SA_C + k * G::SA_F + h * 16;
+        int4 raw[8];  // all eight LDS reads in flight before the first use
+#pragma unroll
+        for (int ky = 0; ky < 8; ky++) raw[ky] = *(const int4*)(src + ky * 32);
+        int qmax = INT32_MIN, qmin = INT32_MAX, tmax = 0, tmin = 0;
+#pragma unroll
+        for (int ky = 0; ky < 8; ky++) {
+            const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
+            int t[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                t[e] = __mul24(vv[e], stp[e + ky]);
+                b[ky][e] = (double)t[e];
+            }
+            qmax = max(qmax, max(max(vv[0], vv[1]), max(vv[2], vv[3])));
+            qmin = min(qmin, min(min(vv[0], vv[1]), min(vv[2], vv[3])));
+            tmax = max(tmax, max(max(t[0], t[1]), max(t[2], t[3])));
+            tmin = min(tmin, min(min(t[0], t[1]), min(t[2], t[3])));
+        }
+        q_range_bad = (qmax > 0x7FFFFF) | (qmin < -0x800000);
+        // float upper bound of amax (nearest rounding is within 2^-24 relative; the product with
+        // 1 + 2^-22 rounds to at least amax): the cube reduction then moves one dword per step
+        amax_f = (float)max(tmax, -tmin) * (1.0f + 0x1p-22f);
+    }
+    after_a();
+    // amax over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
+    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0xB1, 0xF, 0xF, false)));  // quad_perm xor 1
+    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x4E, 0xF, 0xF, false)));  // quad_perm xor 2
+    if constexpr (D == 8)
+        amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+    {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, amax_f), __builtin_bit_cast(uint32_t, amax_f), false, false);
+        amax_f = fmaxf(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+    }
+    const double amax = (double)amax_f;
+
+    // ---- inverse pass Y ----
+    constexpr int G1 = PG == 0 ? 4 : PG;
+#pragma unroll
+    for (int e0 = 0; e0 < 4; e0 += G1) {
+        double col[G1][8];
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int y = 0; y < 8; y++) col[i][y] = b[y][e0 + i];
+        if (PG) for (int i = 0; i < G1; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++) idct8(col[i]);
+        if (PG) for (int i = 0; i < G1; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int y = 0; y < 8; y++) b[y][e0 + i] = col[i][y];
+    }
+
+    // ---- A -> B: swap the off-diagonal 4x4 blocks of the lane pair (l, l^16) ----
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) swap16(b[r][e], b[4 + r][e]);
+    // now row r of this lane (y = 4h + r): x 0..3 in b[r][.], x 4..7 in b[4 + r][.]
+
+    // ---- inverse pass X ----
+#pragma unroll
+    for (int r0 = 0; r0 < 4; r0 += G1) {
+        double row[G1][8];
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                row[i][e] = b[r0 + i][e];
+                row[i][4 + e] = b[4 + r0 + i][e];
+            }
+        if (PG) for (int i = 0; i < G1; i++) pin(row[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++) idct8(row[i]);
+        if (PG) for (int i = 0; i < G1; i++) pin(row[i]);
+#pragma unroll
+        for (int i = 0; i < G1; i++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                b[r0 + i][e] = row[i][e];
+                b[4 + r0 + i][e] = row[i][4 + e];
+            }
+    }
+
+    double cz[D][NXC];
+    dec_b_to_c<D>(b, cz, wl, c, k, h);
+
+    // ---- inverse pass Z ----
+    constexpr int G3 = PG == 0 ? NXC : PG;
+#pragma unroll
+    for (int e0 = 0; e0 < NXC; e0 += G3) {
+        double col[G3][D];
+#pragma unroll
+        for (int i = 0; i < G3; i++)
+#pragma unroll
+            for (int z = 0; z < D; z++) col[i][z] = cz[z][e0 + i];
+        if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G3; i++) idctN<D>(col[i]);
+        if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
+#pragma unroll
+        for (int i = 0; i < G3; i++)
+#pragma unroll
+            for (int z = 0; z < D; z++) cz[z][e0 + i] = col[i][z];
+    }
+
+    // ---- certify, clamp + truncate, store ----
+    // |v - v_java| <= m (dct3d_plan.cpp).  The byte is min(max(0, floor(v)), 255), monotone in v, so it
+    // is Java's byte when floor is constant over [v - m, v + m]: frac(v) >= m and frac(v) + m < 1.  In
+    // the fixed-point view (kFixMagic) lo = frac(v) 2^32 to within 1/2 unit, so with
+    // mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] proves it: (lo - mi) <= 2^32 - 1 - 2 mi
+    // as unsigned.  |v| < 2^19 holds when amax < 2^14: |v| <= amax * sum_k |c(n, k)| <= amax 8^1.5;
+    // a larger amax (never from an encoder of 8-bit frames) sends the cube to the replay.
+    const double m = amax * P.dec_G + P.dec_E;
+    const uint32_t mi = (uint32_t)__builtin_ceil(__fma_rn(m, 0x1p32, 0.5)) + 1u;  // + 1: m's own rounding
+    const uint32_t cert_lim = 0xFFFFFFFFu - 2u * mi;
+    const int y = (D == 8) ? k : (4 * h + k);
+    const int x0 = (D == 8) ? 4 * h : 0;
+    bool flag = q_range_bad | (amax_f >= 16384.0f);
+    uint32_t outw[D][NXC / 4];
+    const uint32_t c255 = 255u;
+#pragma unroll
+    for (int z = 0; z < D; z++) {
+#pragma unroll
+        for (int wd = 0; wd < NXC / 4; wd++) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint64_t fx = __builtin_bit_cast(uint64_t, __dadd_rn(cz[z][4 * wd + e], kFixMagic));
+                const uint32_t tl = fix_floor0((uint32_t)(fx >> 32));
+                flag |= ((uint32_t)fx - mi) > cert_lim;
+                // byte e of w = min(tl, 255) (SDWA byte insert: the other bytes are preserved)
+                if (e == 0) w = min(tl, 255u);
+                else if (e == 1) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
+                else if (e == 2) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
+                else asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
+            }
+            asm volatile("" : "+v"(w));  // one output word at a time (bounded live range)
+            outw[z][wd] = w;
+        }
+    }
+    if (valid) {
+        const uint32_t s = fdiv(g, P.div_cps);
+        const uint32_t rr = g - s * P.cubes_per_stack;
+        const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
+        uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + y) * P.width + bx * 8 + x0;
+#pragma unroll
+        for (int z = 0; z < D; z++) {
+            if constexpr (NXC == 4) *(uint32_t*)(dst + (size_t)z * P.plane) = outw[z][0];
+            else *(uint2*)(dst + (size_t)z * P.plane) = make_uint2(outw[z][0], outw[z][1]);
+        }
+    }
+    // uncertified pixels are rare (tens per 2e9): the cube goes to the whole-cube replay list (one
+    // lane per cube appends it), which keeps the main path free of per-pixel bookkeeping
+    const unsigned long long fl = __ballot(flag && valid);
+    if (__builtin_expect(fl != 0ull, 0)) {
+        const int base = (lane & 32) + ((lane & 15) & ~(D - 1));
+        const unsigned long long cmask = ((unsigned long long)((1u << D) - 1) << base) |
+                                         ((unsigned long long)((1u << D) - 1) << (base + 16));
+        if ((fl & cmask) != 0ull && (int)__builtin_ctzll(fl & cmask) == lane) {
+            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
+            P.cube_list[idx] = g;
+        }
+    }
+}
+
+template <int D, int PG>
+__global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
+    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    char* wl = lds + wave * kDecWaveLds;
+    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * DecGeom<D>::CPW;
+    int4 v[8];
+    dec_load_tile<D>(P, cube0, lane, v);
+    dec_stage_tile<D>(wl, lane, v);
+    wave_lds_sync();
+    decode_tile<D, PG>(P, wl, lane, cube0, [] {});
+}
+
+}  // namespace dct3d

@@ -109,7 +109,6 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st);
 // true when launch_encode(D) replays uncertified coefficients itself (encode16_kernel: 8x8x8), i.e. the
 // call needs no counter reset and no encode_fixup_kernel
 bool encode_replays_inwave(int D);
-int launch_encode_memonly(int D, const EncodeParams& P, hipStream_t st);  // diagnostic
 int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
 struct EgParams {
     const int32_t* q;          // cube-major quantised values
@@ -158,23 +157,11 @@ struct EgFusedParams {
                                // first bit at bit 31 of its word 0
     uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
     uint16_t* lane_bits;       // [n_seg * 64] bits coded by each lane
-    uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input; single pass: the stitch's)
-    // single pass (encode_eg_kernel<D, true>): each wave places its segment in the stream itself,
-    // its offset from a decoupled look-back over the preceding segments (no slot, scan or compaction)
-    uint64_t* seg_state;       // [n_seg] look-back words, zeroed per call: bit 63 inclusive prefix,
-                               // bit 62 aggregate (bits 0..61 the value), both = this segment gave up
-    uint64_t* seg_off;         // [n_seg] stream bit offset of each segment (carry included)
-    uint32_t* head;            // [n_seg] first / last output word of each segment (eg_stitch_kernel)
-    uint32_t* tail;
-    uint32_t* out;             // output words (memory byte order)
-    uint64_t out_cap_words;
-    uint64_t* status;          // [0] total bits (carry included), [1] 1: capacity, 4: look-back gave up
-    uint32_t carry_bits;
+    uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
 };
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
-// single_pass: the look-back variant (E.seg_state zeroed; eg_stitch afterwards, no compaction)
-int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, bool single_pass, hipStream_t st);
+int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st);
 int launch_eg_stitch(const EgParams& P, hipStream_t st);
 // scan of the segment bits + the lanes' words concatenated into the stream + stitch (P.n_cubes =
 // segments, P.bits = seg_bits)
@@ -192,8 +179,5 @@ int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st);
 // fused stream -> raster decode: values parsed at the marks straight into the decode's LDS staging
 int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st);
 int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
-int launch_ceiling(const uint8_t* in, uint8_t* out, long long n_px, int mode, unsigned* sink, hipStream_t st);
-int launch_synth(uint8_t* out, int width, int height, long long n_pix, uint64_t seed, long long frame0, int kind,
-                 hipStream_t st);
 
 }  // namespace dct3d

@@ -65,7 +65,7 @@ struct dct3d_ctx {
     // test / diagnostic options (dct3d_ctx_set_option): how later calls reach their results
     uint32_t opt_flag_cap = 0;      // 0: default capacity
     double opt_dec_margin = 0.0;    // added to the decode margin
-    bool opt_enc_no_recheck = false, opt_eg_single_pass = false, opt_eg_two_step = false,
+    bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
     // certify-or-replay state
     DevBuf d_flags, d_cubes, d_counters;
@@ -84,7 +84,7 @@ struct dct3d_ctx {
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
     // fused encode + Exp-Golomb: per-segment slots and lane bit counts
-    DevBuf d_egf_slot, d_egf_lbits, d_egf_state;
+    DevBuf d_egf_slot, d_egf_lbits;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
@@ -244,7 +244,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
                       &c->d_cubes, &c->d_counters, &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egf_slot,
-                      &c->d_egf_lbits, &c->d_egf_state})
+                      &c->d_egf_lbits})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -265,6 +265,14 @@ int dct3d_ctx_set_stream(dct3d_ctx* c, void* s) {
     return DCT3D_OK;
 }
 
+int dct3d_ctx_info(const dct3d_ctx* c, int* device, int* block_d, void** hip_stream) {
+    if (!c) return DCT3D_EINVAL;
+    if (device) *device = c->device;
+    if (block_d) *block_d = c->bd;
+    if (hip_stream) *hip_stream = (void*)c->stream;
+    return DCT3D_OK;
+}
+
 int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
     if (!c || !(value >= 0.0)) return DCT3D_EINVAL;
     switch (option) {
@@ -274,7 +282,6 @@ int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
             return DCT3D_OK;
         case DCT3D_OPT_DEC_MARGIN: c->opt_dec_margin = value; return DCT3D_OK;
         case DCT3D_OPT_ENC_NO_RECHECK: c->opt_enc_no_recheck = value != 0.0; return DCT3D_OK;
-        case DCT3D_OPT_EG_SINGLE_PASS: c->opt_eg_single_pass = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
         default: return DCT3D_EINVAL;
@@ -486,26 +493,6 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     c->last_valid = true;
     if (d_dct) return forward_f64_raster(c, d_raster, w, h, n_cubes, d_dct);
     return DCT3D_OK;
-}
-
-int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q) {
-    if (!c || (!d_raster && n_stacks) || (!d_q && n_stacks)) return DCT3D_EINVAL;
-    uint64_t n_cubes;
-    int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
-    if (rc) return rc;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    EncodeParams P;
-    memset(&P, 0, sizeof(P));
-    P.raster = d_raster;
-    P.out = d_q;
-    P.n_cubes = (uint32_t)n_cubes;
-    P.cubes_per_stack = (uint32_t)((w / 8) * (h / 8));
-    P.nbx = (uint32_t)(w / 8);
-    set_fast_div(P);
-    P.width = (uint32_t)w;
-    P.plane = (uint64_t)w * h;
-    P.stack_stride = P.plane * c->bd;
-    return launch_encode_memonly(c->bd, P, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
 }
 
 int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_stacks, uint8_t* d_raster) {
@@ -770,20 +757,6 @@ int dct3d_inverse_f32(dct3d_ctx* c, const float* in, size_t n_cubes, float* out)
     return cube_f32_host(c, in, n_cubes, out, true);
 }
 
-int dct3d_bandwidth_probe_dev(dct3d_ctx* c, const uint8_t* d_in, void* d_out, size_t n_px, int mode) {
-    if (!c || n_px % 16 || mode < 0 || mode > 5 || (mode != 2 && mode != 5 && !d_in) || (mode != 3 && !d_out)) return DCT3D_EINVAL;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    return launch_ceiling(d_in, (uint8_t*)d_out, (long long)n_px, mode, (unsigned*)c->d_counters.p, c->stream)
-               ? DCT3D_EKERNEL : DCT3D_OK;
-}
-
-int dct3d_fill_synthetic_dev(dct3d_ctx* c, uint8_t* d, int w, int h, int n_frames, uint64_t seed, int64_t frame0,
-                             int kind) {
-    if (!c || !d || w <= 0 || h <= 0 || n_frames < 0 || (kind != 0 && kind != 1)) return DCT3D_EINVAL;
-    if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    return launch_synth(d, w, h, (long long)w * h * n_frames, seed, frame0, kind, c->stream) ? DCT3D_EKERNEL : DCT3D_OK;
-}
-
 // ---- Exp-Golomb stage ----------------------------------------------------------------------------
 int dct3d_diagonal_order(int bw, int bh, int bd, uint16_t* out) {
     if (!out || bw != 8 || bh != 8 || (bd != 8 && bd != 4)) return DCT3D_EINVAL;
@@ -857,13 +830,10 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     const uint64_t n_seg = (n_cubes + 7) / 8, n_chunks = (n_seg + 4095) / 4096;
     // worst case per lane: cs/8 values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 14 bits)
     const uint32_t seg_cap = (uint32_t)(64 * (((c->plan.cs / 8) * 27 + 31) / 32));
-    // two passes (the default): K1 codes into per-segment slots, then scan + compaction.  The single pass
-    // (DCT3D_OPT_EG_SINGLE_PASS: K1 places the stream itself after a decoupled look-back) writes the same
-    // stream but measured slower; a look-back that gives up falls back to two passes
-    bool sp = c->opt_eg_single_pass;
-    if ((rc = sp ? c->d_egf_state.grow(n_seg * sizeof(uint64_t)) : 0) ||
-        (rc = sp ? 0 : c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
-        (rc = sp ? 0 : c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
+    // two passes: K1 codes into per-segment slots, then scan + compaction (a single pass by decoupled
+    // look-back wrote the same stream but measured slower: DESIGN.md §4b)
+    if ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
+        (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
         (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
         (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
         return rc;
@@ -894,14 +864,6 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     E.seg_cap = seg_cap;
     E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
     E.seg_bits = (uint32_t*)c->d_eg_bits.p;
-    E.seg_state = (uint64_t*)c->d_egf_state.p;
-    E.seg_off = (uint64_t*)c->d_eg_off.p;
-    E.head = (uint32_t*)c->d_eg_ht.p;
-    E.tail = (uint32_t*)c->d_eg_ht.p + n_seg;
-    E.out = (uint32_t*)d_out;
-    E.out_cap_words = out_cap / 4;
-    E.status = (uint64_t*)c->d_eg_status.p;
-    E.carry_bits = (uint32_t)carry_bits;
     EgParams G;
     G.q = nullptr;
     G.n_cubes = n_seg;  // segments
@@ -917,32 +879,16 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     G.carry_bits = (uint32_t)carry_bits;
     G.carry_byte = carry_byte;
     uint64_t st[2] = {0, 0};
-    for (;;) {
-        if (!sp && ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
-                    (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t)))))
-            return rc;
-        E.slot = (uint32_t*)c->d_egf_slot.p;
-        E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
-        if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess ||
-            (sp && hipMemsetAsync(c->d_egf_state.p, 0, n_seg * sizeof(uint64_t), c->stream) != hipSuccess))
-            return DCT3D_EDEVICE;
-        hipEvent_t* ev = timing_slot(c);
-        if (ev) (void)hipEventRecord(ev[0], c->stream);
-        if (launch_encode_eg(D, P, E, sp, c->stream)) return DCT3D_EKERNEL;
-        if (ev) (void)hipEventRecord(ev[1], c->stream);
-        if (ev) (void)hipEventRecord(ev[2], c->stream);
-        if (sp ? launch_eg_stitch(G, c->stream) : launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream))
-            return DCT3D_EKERNEL;
-        if (ev) (void)hipEventRecord(ev[3], c->stream);
-        if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipStreamSynchronize(c->stream) != hipSuccess)
-            return DCT3D_EDEVICE;
-        if (sp && (st[1] & 4)) {  // a look-back gave up (never expected): the two-pass path
-            sp = false;
-            continue;
-        }
-        break;
-    }
+    hipEvent_t* ev = timing_slot(c);
+    if (ev) (void)hipEventRecord(ev[0], c->stream);
+    if (launch_encode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[1], c->stream);
+    if (ev) (void)hipEventRecord(ev[2], c->stream);
+    if (launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream)) return DCT3D_EKERNEL;
+    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     if (st[1] & 1) return DCT3D_ENOSPC;

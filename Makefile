@@ -15,16 +15,18 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall 
 CFLAGS   := -O2 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude -std=c11 -D_GNU_SOURCE
 
 DEV_SRCS  := $(CSRC)/dct3d_kernels.hip $(CSRC)/dct3d_kernels_f.hip $(CSRC)/dct3d_eg.hip
+DIAG_SRCS := $(CSRC)/dct3d_diag.hip
 HOST_SRCS := $(CSRC)/dct3d_plan.cpp $(CSRC)/dct3d_runtime.cpp
-HDRS      := $(wildcard $(CSRC)/*.h) include/dct3d.h
+HDRS      := $(wildcard $(CSRC)/*.h) include/dct3d.h include/dct3d_diag.h
 CODEC_SRCS := $(wildcard $(CSRC)/host/*.c)
 CODEC_LIB_SRCS := $(filter-out $(CSRC)/host/main.c,$(CODEC_SRCS))
 
 LIB      := $(LIBDIR)/libdct3d.so
+DIAGLIB  := $(LIBDIR)/libdct3d_diag.so
 CODECLIB := $(LIBDIR)/libdct3dcodec.so
 CLI      := $(LIBDIR)/dct3d_codec
 
-all: $(LIB) $(if $(CODEC_LIB_SRCS),$(CODECLIB) $(CLI))
+all: $(LIB) $(DIAGLIB) $(if $(CODEC_LIB_SRCS),$(CODECLIB) $(CLI))
 
 $(OBJ)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -37,6 +39,10 @@ $(OBJ)/%.o: $(CSRC)/%.cpp $(HDRS)
 $(LIB): $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(DEV_SRCS)) $(patsubst $(CSRC)/%.cpp,$(OBJ)/%.o,$(HOST_SRCS))
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+# measurement / test support (include/dct3d_diag.h): never linked into the product library
+$(DIAGLIB): $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(DIAG_SRCS)) $(LIB)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(DIAG_SRCS)) -L$(LIBDIR) -ldct3d -Wl,-rpath,'$$ORIGIN'
 
 $(CODECLIB): $(CODEC_LIB_SRCS) $(LIB) $(wildcard include/*.h)
 	@mkdir -p $(LIBDIR)

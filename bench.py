@@ -184,13 +184,31 @@ def pmc_traffic(config: str, kernel: str, depth: int):
     return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
 
 
-def measure_ceiling(ctx, torch, frames, q, reps, geom=None):
+def measure_ceiling(ctx, torch, frames, q, reps, geom=None, dec_geom=None):
     """Achievable HBM rates on this device for the path's traffic mix, same buffers, same stream:
     mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only.
     geom = (width, height, stacks, bytes_per_cube) for encode configs: also the encode kernel's own
-    traffic without its compute (dct3d_encode_memonly_dev: same loads, LDS staging, NT stores)."""
+    traffic without its compute (dct3d_encode_memonly_dev: same loads, LDS staging, NT stores).
+    dec_geom = (width, height, stacks, raster_out) for the 8x8x8 decode: its memory part and its compute
+    part alone (dct3d_decode_diag_dev modes 1 / 2; libdct3d_diag.so)."""
     n_px = frames.numel() // 16 * 16
     out = {}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+
+    if dec_geom is not None:
+        width, height, stacks, raster = dec_geom
+        out["decode_memonly_ms"] = timed(lambda: ctx.decode_diag_dev(q, width, height, stacks, raster, 1))
+        out["decode_computeonly_ms"] = timed(lambda: ctx.decode_diag_dev(q, width, height, stacks, raster, 2))
     if geom is not None:
         width, height, stacks, bpc = geom
         ctx.encode_memonly_dev(frames, width, height, stacks, q)
@@ -414,7 +432,8 @@ def main():
                       "psnr_db": (10.0 * math.log10(255.0 ** 2 / mse)) if mse > 0 else None}
     ceiling = None if a.no_ceiling or q is None or not stacks else measure_ceiling(
         ctx, torch, frames, q, max(3, a.steps // 2),
-        geom=(width, height, stacks, cs * 5) if direction == "encode" else None)
+        geom=(width, height, stacks, cs * 5) if direction == "encode" else None,
+        dec_geom=(width, height, stacks, torch.empty_like(frames)) if direction == "decode" and depth == 8 else None)
 
     bytes_per_cube = cs * (1 + 4)  # u8 in + int32 out (encode) / int32 in + u8 out (decode)
     if direction in ("forward_f32", "inverse_f32"):
@@ -433,6 +452,8 @@ def main():
     if ceiling and "encode_memonly_GBs" in ceiling:  # the kernel against its own traffic without compute
         ceiling["kernel_vs_memonly"] = kernel_achieved / ceiling["encode_memonly_GBs"]
         ceiling["step_vs_memonly"] = achieved / ceiling["encode_memonly_GBs"]
+    if ceiling and "decode_memonly_ms" in ceiling and kernel_ms > 0:
+        ceiling["kernel_vs_memonly"] = ceiling["decode_memonly_ms"] / kernel_ms
     kname = ("decode_eg_kernel" if fused_dec else "decode_kernel") if direction in ("decode", "decode_eg") else (
         "encode_eg_kernel" if fused else ("encode16_kernel" if depth == 8 else "encode_kernel"))
     if direction in ("forward_f32", "inverse_f32"):

@@ -60,7 +60,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written past its end) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 5
+#define DCT3D_ABI_VERSION 6
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -114,6 +114,9 @@ void dct3d_ctx_destroy(dct3d_ctx *ctx);
 /* Use an external hipStream_t (e.g. a framework's current stream) instead of the ctx-owned one.
  * NULL restores the ctx-owned stream. */
 int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
+/* The ctx's device ordinal, block depth and the hipStream_t its calls run on (any pointer may be
+ * NULL).  Lets companion libraries (libdct3d_diag.so) queue work in order with the ctx's. */
+int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_stream);
 /* Test / diagnostic options of a ctx.  Each one changes only HOW later calls reach their results
  * (the results stay bit-identical): tests use them to drive the rare paths.  value 0 restores the
  * default.  Unknown options: DCT3D_EINVAL. */
@@ -122,7 +125,6 @@ int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
 #define DCT3D_OPT_DEC_MARGIN 2        /* added to the decode certification margin: cubes go to the replay */
 #define DCT3D_OPT_ENC_NO_RECHECK 3    /* 1: the 8x8x8 encode skips its fp64 second certificate, so every
                                          coefficient the fp32 certificate leaves open takes the Java fold */
-#define DCT3D_OPT_EG_SINGLE_PASS 4    /* 1: fused encode + Exp-Golomb by decoupled look-back (one pass) */
 #define DCT3D_OPT_EG_TWO_STEP 5       /* 1: dct3d_encode_eg / dct3d_decode_eg through int32 cubes */
 #define DCT3D_OPT_EG_NO_RESOLVE 6     /* 1: Exp-Golomb decode sync by plain confirming passes only */
 int dct3d_ctx_set_option(dct3d_ctx *ctx, int option, double value);
@@ -165,29 +167,6 @@ int dct3d_forward_f32(dct3d_ctx *ctx, const float *cubes, size_t n_cubes, float 
 int dct3d_inverse_f32(dct3d_ctx *ctx, const float *coeffs, size_t n_cubes, float *pixels);
 int dct3d_forward_f32_dev(dct3d_ctx *ctx, const float *d_cubes, size_t n_cubes, float *d_coeffs);
 int dct3d_inverse_f32_dev(dct3d_ctx *ctx, const float *d_coeffs, size_t n_cubes, float *d_pixels);
-
-/* ---------------------------------------------------------------------------------------------
- * Benchmark / test support: integer-only deterministic synthetic frames, identical to the
- * Python generator (3ddctvideoencoding_amd.synthetic).  For global pixel index
- * idx = ((frame0 + f) * height + y) * width + x:
- *   kind 0 ("ramp"):    clamp(128 + ((3x + 5y + 7(frame0+f)) & 63) - 32 + (splitmix64(seed ^ idx) & 15))
- *   kind 1 ("uniform"): splitmix64(seed ^ idx) & 255
- * ------------------------------------------------------------------------------------------- */
-int dct3d_fill_synthetic_dev(dct3d_ctx *ctx, uint8_t *d_frames, int width, int height, int n_frames,
-                             uint64_t seed, int64_t frame0, int kind);
-
-/* Bandwidth calibration (bench support): the encode's traffic pattern without the transform, on the
- * context stream.  mode 0: d_in u8 [n_px] -> d_out int32 [n_px] (1 B read : 4 B written, NT stores);
- * mode 1: copy n_px bytes; mode 2: write 4*n_px bytes; mode 3: read n_px bytes; modes 4/5: copy /
- * write with plain (temporal) stores.  n_px % 16 == 0. */
-int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, size_t n_px, int mode);
-
-/* Memory-only twin of dct3d_encode_stacks_dev (bench support; d_q receives NOT a DCT): the encode
- * kernel's row loads, LDS staging and 1 KiB non-temporal stores of the same cubes, without the
- * transform, quantisation, certification or fixup.  Its rate is the ceiling the encode's own traffic
- * reaches on this device. */
-int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
-                             int32_t *d_q);
 
 /* ---- Exp-Golomb stage on the device -----------------------------------------
  * Replaces applyExpGolombCoding (encoder.c:60-71) over expGolomb_writeValue (ExpGolomb.c:32-64) /

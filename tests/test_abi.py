@@ -33,6 +33,16 @@ def test_dct3d_header_symbols_exported(pkg):
     assert set(pkg.ABI_SYMBOLS) <= set(names)
 
 
+def test_diag_header_symbols_exported_by_diag_lib_only(pkg):
+    """include/dct3d_diag.h (measurement / test support) is exported by libdct3d_diag.so and by
+    nothing in the product library."""
+    names = _declared("dct3d_diag.h")
+    exp = _exported(pkg.DIAG_LIB_PATH)
+    assert not [n for n in names if n not in exp]
+    assert set(pkg.DIAG_SYMBOLS) == set(names)
+    assert not set(names) & _exported(pkg.LIB_PATH)
+
+
 @pytest.mark.parametrize("header", ["codec.h", "cube_utils.h", "exp_golomb.h", "cube_io.h"])
 def test_codec_header_symbols_exported(pkg, header):
     names = _declared(header)

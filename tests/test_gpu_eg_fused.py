@@ -66,15 +66,14 @@ def test_fused_ragged_segment_tails(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("w,h,stacks", [(8, 8, 1), (40, 8, 5), (136, 72, 2)])
 @pytest.mark.parametrize("carry_bits", [0, 3])
-def test_fused_single_pass_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, w, h,
-                                          stacks, carry_bits):
-    """DCT3D_OPT_EG_SINGLE_PASS on small and ragged inputs (one segment, a partial last segment, the
-    carried byte taken by segment 0's look-back) against the oracle's stream"""
+def test_fused_ragged_carry_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, w, h,
+                                           stacks, carry_bits):
+    """small and ragged inputs (one segment, a partial last segment) continuing a carried partial byte,
+    against the oracle's stream; nothing is written past the stream's last word"""
     ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
     fr = pkg.synthetic.frames(w, h, stacks * depth, kind="uniform", frame0=w + carry_bits)
     exp, ebits = _expected(oracle, pkg, plan.encode_q(fr), depth, 0x3C, carry_bits)
-    with ctx_option(ctx, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1):
-        got, tb, raw = _fused(ctx, fr, 0x3C, carry_bits)
+    got, tb, raw = _fused(ctx, fr, 0x3C, carry_bits)
     assert tb == ebits and got == exp
     assert not raw[len(got):(tb + 31) // 32 * 4].any()
 
@@ -110,26 +109,19 @@ def test_fused_1080p_matches_oracle(pkg, oracle, plan8, gpu_ctx8):
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("kind", ["uniform", "checker"])
 @pytest.mark.parametrize("carry_bits", [0, 5])
-def test_fused_single_pass_matches_two_pass(pkg, gpu_ctx8, gpu_ctx4, depth, kind, carry_bits):
-    """DCT3D_OPT_EG_SINGLE_PASS (each wave places its bits after a decoupled look-back over the earlier
-    segments' totals) and the default two passes (slots + scan + compaction) write the same stream;
-    1080p x 3 stacks is ~49k segments, so look-backs run across many waves still in flight"""
+def test_fused_matches_two_step_carry(pkg, gpu_ctx8, gpu_ctx4, depth, kind, carry_bits):
+    """the fused path (slots + scan + compaction) and the two-step path (int32 cubes, then the
+    stand-alone Exp-Golomb stage) write the same stream at 1080p x 3 stacks (~49k segments) with a
+    carried partial byte, on uniform noise and on a checkerboard (long codes everywhere)"""
     ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
     fr = _content(pkg, kind, 1920, 1080, 3 * depth) if kind != "uniform" else \
         pkg.synthetic.frames(1920, 1080, 3 * depth, kind="uniform", frame0=11)
     tp, ttp, _ = _fused(ctx, fr, 0xA5, carry_bits)
-    with ctx_option(ctx, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1):
-        sp, tsp, _ = _fused(ctx, fr, 0xA5, carry_bits)
-    assert tsp == ttp and sp == tp
+    ref, rbits, _ = _gpu_stream(ctx, ctx.encode_stacks(fr), 0xA5, carry_bits)
+    assert ttp == rbits and tp == ref
 
 
-@pytest.mark.parametrize("single_pass", [False, True])
-def test_fused_capacity(pkg, gpu_ctx8, single_pass):
-    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_SINGLE_PASS, 1 if single_pass else 0):
-        _fused_capacity(pkg, gpu_ctx8, single_pass)
-
-
-def _fused_capacity(pkg, gpu_ctx8, single_pass):
+def test_fused_capacity(pkg, gpu_ctx8):
     fr = pkg.synthetic.frames(64, 64, 8, kind="uniform")
     _, tb, _ = _fused(gpu_ctx8, fr)
     import torch
@@ -140,8 +132,7 @@ def _fused_capacity(pkg, gpu_ctx8, single_pass):
         gpu_ctx8.encode_eg_dev(d, 64, 64, 1, out, small)
     assert ei.value.code == pkg.DCT3D_ENOSPC
     o = out.cpu().numpy()
-    assert (o[small // 4:] == 7).all()             # nothing written past out_cap
-    assert single_pass or (o == 7).all()           # two passes: nothing written at all
+    assert (o == 7).all()                          # nothing written at all
     got, tb2, _ = _fused(gpu_ctx8, fr, cap=(tb + 31) // 32 * 4)   # exactly enough
     assert tb2 == tb
 
