@@ -157,12 +157,63 @@ __device__ __forceinline__ void dec_b_to_c(const double (&b)[8][4], double (&cz)
     }
 }
 
+// ---- exact replay of one uncertified cube (InverseDCT.java:56-66 / Decoder.java:107-117: for each pixel,
+//      k ascending, zero coefficients skipped, acc = acc + c_k * coef[n][k] with both operations rounded,
+//      then clamp to [0, 255] and the (int) / (byte) truncation).  The whole wave: reload() puts the
+//      cube's dequantised coefficients in LDS (cf[k] = q_k * step_k, exact), lane l folds pixels
+//      l + 64 i reading the transposed table (coalesced, L2-resident), and the bytes land in LDS after
+//      cf.  Not inlined: the main path's register allocation stays its own. ----
+template <int D>
+struct ReloadCubes {  // from the int32 cube-major input
+    const int32_t* in;
+    __device__ __forceinline__ void operator()(uint32_t g, double* cf, int lane) const {
+        constexpr int CS = 64 * D;
+#pragma unroll
+        for (int i = 0; i < CS / 64; i++) {
+            const int k = lane + 64 * i;
+            const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+            cf[k] = (double)in[(size_t)g * CS + k] * (double)max(1, 5 * (kx + ky + kz));
+        }
+    }
+};
+
+template <int D, class Reload>
+__device__ __attribute__((noinline)) const uint8_t* decode_replay_cube(const double* inv_coef_t, Reload reload,
+                                                                       char* wl, int lane, uint32_t g) {
+    constexpr int CS = 64 * D, NP = CS / 64;
+    static_assert(CS * 8 + CS <= kDecWaveLds, "replay scratch fits the wave's region");
+    double* cf = (double*)wl;
+    uint8_t* ob = (uint8_t*)(wl + CS * 8);
+    wave_lds_sync();
+    reload(g, cf, lane);
+    wave_lds_sync();
+    double acc[NP];
+#pragma unroll
+    for (int i = 0; i < NP; i++) acc[i] = 0.0;
+    const double* tab = inv_coef_t + lane;
+    for (int k = 0; k < CS; k++) {
+        const double cv = cf[k];  // the same word for every lane: a uniform branch
+        if (cv != 0.0) {
+#pragma unroll
+            for (int i = 0; i < NP; i++) acc[i] = __dadd_rn(acc[i], __dmul_rn(cv, tab[(size_t)k * CS + 64 * i]));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        const double mn = acc[i] < 255.0 ? acc[i] : 255.0;
+        ob[lane + 64 * i] = (uint8_t)(int)(mn > 0.0 ? mn : 0.0);
+    }
+    wave_lds_sync();
+    return ob;
+}
+
 // One tile (CPW cubes) from the staged input in the wave's LDS region to the raster.  after_a() runs
-// once the staged input is in registers (the persistent variant issues the next tile's loads there).
+// once the staged input is in registers (the persistent variant issues the next tile's loads there);
+// reload(g, cf, lane) re-reads cube g's dequantised coefficients for the rare exact replay.
 // PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
-template <int D, int PG, class AfterA>
+template <int D, int PG, class AfterA, class Reload>
 __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
-                                            AfterA&& after_a) {
+                                            AfterA&& after_a, const Reload& reload) {
     using G = DecGeom<D>;
     constexpr int CPW = G::CPW;
     constexpr int NXC = (D == 8) ? 4 : 8;  // x values per lane in layout C
@@ -173,9 +224,12 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     const bool valid = g < P.n_cubes;
 
     // ---- layout A: dequantise, amax ----
-    // cf = q * step exactly: a 24-bit integer multiply (|q| < 2^23 checked; |q * step| < 2^30), then
-    // an exact conversion to fp64.  Out-of-range q (never produced by the encoder) sends the cube to
-    // the exact replay.  amax = max |q * step| from integer max / min.
+    // cf = q * step exactly: a 24-bit integer multiply, then an exact conversion to fp64.  One integer
+    // max / min pass over q bounds everything: with M = max(q, ~q) over the lane's values other than
+    // slot (ky, e) = (0, 0), |q| <= M + 1, so |q * step| <= (M + 1) * (sb + 50) (the lane's largest
+    // step); slot (0, 0) (the DC on the DC lane, step 1) enters as its exact product t00.  Any |q| >=
+    // 2^15 (never produced by an encoder of 8-bit frames) sends the cube to the exact replay, which
+    // also keeps the 24-bit products exact.
     double b[8][4];
     float amax_f;
     bool q_range_bad;
@@ -189,25 +243,26 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         int4 raw[8];  // all eight LDS reads in flight before the first use
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) raw[ky] = *(const int4*)(src + ky * 32);
-        int qmax = INT32_MIN, qmin = INT32_MAX, tmax = 0, tmin = 0;
+        int qmax = max(raw[0].y, max(raw[0].z, raw[0].w)), qmin = min(raw[0].y, min(raw[0].z, raw[0].w));
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) {
             const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
-            int t[4];
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                t[e] = __mul24(vv[e], stp[e + ky]);
-                b[ky][e] = (double)t[e];
+            for (int e = 0; e < 4; e++) b[ky][e] = (double)__mul24(vv[e], stp[e + ky]);
+            if (ky) {
+                qmax = max(qmax, max(max(vv[0], vv[1]), max(vv[2], vv[3])));
+                qmin = min(qmin, min(min(vv[0], vv[1]), min(vv[2], vv[3])));
             }
-            qmax = max(qmax, max(max(vv[0], vv[1]), max(vv[2], vv[3])));
-            qmin = min(qmin, min(min(vv[0], vv[1]), min(vv[2], vv[3])));
-            tmax = max(tmax, max(max(t[0], t[1]), max(t[2], t[3])));
-            tmin = min(tmin, min(min(t[0], t[1]), min(t[2], t[3])));
         }
-        q_range_bad = (qmax > 0x7FFFFF) | (qmin < -0x800000);
+        const int q00 = raw[0].x;
+        const int mq = max(qmax, ~qmin);      // >= |q| - 1 over the 31 values
+        const int m00 = max(q00, ~q00);       // >= |q00| - 1
+        q_range_bad = max(mq, m00) >= 0x8000;
+        const int t00 = __mul24(q00, stp[0]);
+        const uint32_t amax_i = max((uint32_t)max(t00, -t00), __umul24((uint32_t)mq + 1u, (uint32_t)(sb + 50)));
         // float upper bound of amax (nearest rounding is within 2^-24 relative; the product with
         // 1 + 2^-22 rounds to at least amax): the cube reduction then moves one dword per step
-        amax_f = (float)max(tmax, -tmin) * (1.0f + 0x1p-22f);
+        amax_f = (float)amax_i * (1.0f + 0x1p-22f);
     }
     after_a();
     // amax over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
@@ -296,16 +351,20 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     // ---- certify, clamp + truncate, store ----
     // |v - v_java| <= m (dct3d_plan.cpp).  The byte is min(max(0, floor(v)), 255), monotone in v, so it
     // is Java's byte when floor is constant over [v - m, v + m]: frac(v) >= m and frac(v) + m < 1.  In
-    // the fixed-point view (kFixMagic) lo = frac(v) 2^32 to within 1/2 unit, so with
-    // mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] proves it: (lo - mi) <= 2^32 - 1 - 2 mi
-    // as unsigned.  |v| < 2^19 holds when amax < 2^14: |v| <= amax * sum_k |c(n, k)| <= amax 8^1.5;
-    // a larger amax (never from an encoder of 8-bit frames) sends the cube to the replay.
-    const double m = amax * P.dec_G + P.dec_E;
+    // the fixed-point view (kFixMagic, |v| < 2^19) lo = frac(v) 2^32 to within 1/2 unit, so with
+    // mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] for every pixel proves it: the lane keeps
+    // min and max of lo (one v_min3 / v_max3 per two pixels) and tests them once.
+    // Range: |v| <= amax * sum_k |c(n, k)| <= 18.4 amax (8^1.5 bounds the sum), so amax < 2^16 gives
+    // |v| < 1.21e6 < 1.5 * 2^20 = kFixMagic: w = v + kFixMagic > 0.  For |v| >= 2^19 the view is not
+    // fixed point, but the byte still is Java's: w >= 2^21 has a high word above kFixHi + 255 (-> 255,
+    // and v_java > 2^19 - m > 255), w < 2^20 one below kFixHi (-> 0, and v_java < 0), whatever the
+    // certificate then says.  amax >= 2^16 (never from an encoder of 8-bit frames) goes to the replay.
+    const double m = __builtin_fmin(amax * P.dec_G + P.dec_E, 0.5);
     const uint32_t mi = (uint32_t)__builtin_ceil(__fma_rn(m, 0x1p32, 0.5)) + 1u;  // + 1: m's own rounding
-    const uint32_t cert_lim = 0xFFFFFFFFu - 2u * mi;
     const int y = (D == 8) ? k : (4 * h + k);
     const int x0 = (D == 8) ? 4 * h : 0;
-    bool flag = q_range_bad | (amax_f >= 16384.0f);
+    bool flag = q_range_bad | (amax_f >= 65536.0f);
+    uint32_t lo_min = 0xFFFFFFFFu, lo_max = 0u;
     uint32_t outw[D][NXC / 4];
     const uint32_t c255 = 255u;
 #pragma unroll
@@ -317,7 +376,8 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             for (int e = 0; e < 4; e++) {
                 const uint64_t fx = __builtin_bit_cast(uint64_t, __dadd_rn(cz[z][4 * wd + e], kFixMagic));
                 const uint32_t tl = fix_floor0((uint32_t)(fx >> 32));
-                flag |= ((uint32_t)fx - mi) > cert_lim;
+                lo_min = min(lo_min, (uint32_t)fx);
+                lo_max = max(lo_max, (uint32_t)fx);
                 // byte e of w = min(tl, 255) (SDWA byte insert: the other bytes are preserved)
                 if (e == 0) w = min(tl, 255u);
                 else if (e == 1) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
@@ -328,28 +388,49 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             outw[z][wd] = w;
         }
     }
+    flag |= (lo_min < mi) | (lo_max > 0xFFFFFFFFu - mi);
+    // ---- rare path: uncertified cubes (tens per 2e9 pixels) are replayed whole by the wave, before
+    //      the stores: the exact Java fold writes the cube's bytes to LDS and the owning lanes take
+    //      their words from there (no second store of any address, no flag list, no fixup launch) ----
+    const unsigned long long fl = __ballot(flag && valid);
+    if (__builtin_expect(fl != 0ull, 0)) {
+        uint32_t nrep = 0;
+        for (int ci = 0; ci < CPW; ci++) {
+            const int base = (ci / (CPW / 2)) * 32 + (ci % (CPW / 2)) * D;
+            const unsigned long long cmask = ((unsigned long long)((1u << D) - 1) << base) |
+                                             ((unsigned long long)((1u << D) - 1) << (base + 16));
+            if ((fl & cmask) == 0ull) continue;  // wave-uniform
+            const uint8_t* ob = decode_replay_cube<D>(P.inv_coef_t, reload, wl, lane, cube0 + ci);
+            if (c == ci) {
+#pragma unroll
+                for (int z = 0; z < D; z++)
+#pragma unroll
+                    for (int wd = 0; wd < NXC / 4; wd++) outw[z][wd] = *(const uint32_t*)(ob + z * 64 + y * 8 + x0 + 4 * wd);
+            }
+            wave_lds_sync();
+            nrep++;
+        }
+        if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
+    }
     if (valid) {
         const uint32_t s = fdiv(g, P.div_cps);
         const uint32_t rr = g - s * P.cubes_per_stack;
         const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
         uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + y) * P.width + bx * 8 + x0;
 #pragma unroll
-        for (int z = 0; z < D; z++) {
-            if constexpr (NXC == 4) *(uint32_t*)(dst + (size_t)z * P.plane) = outw[z][0];
-            else *(uint2*)(dst + (size_t)z * P.plane) = make_uint2(outw[z][0], outw[z][1]);
+        for (int z = 0; z < D; z++, dst += P.plane) {  // one 64-bit add per plane
+            if constexpr (NXC == 4) *(uint32_t*)dst = outw[z][0];
+            else *(uint2*)dst = make_uint2(outw[z][0], outw[z][1]);
         }
     }
-    // uncertified pixels are rare (tens per 2e9): the cube goes to the whole-cube replay list (one
-    // lane per cube appends it), which keeps the main path free of per-pixel bookkeeping
-    const unsigned long long fl = __ballot(flag && valid);
-    if (__builtin_expect(fl != 0ull, 0)) {
-        const int base = (lane & 32) + ((lane & 15) & ~(D - 1));
-        const unsigned long long cmask = ((unsigned long long)((1u << D) - 1) << base) |
-                                         ((unsigned long long)((1u << D) - 1) << (base + 16));
-        if ((fl & cmask) != 0ull && (int)__builtin_ctzll(fl & cmask) == lane) {
-            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-            P.cube_list[idx] = g;
-        }
+}
+
+// Block 0 zeroes the next call's counter slot, both halves (the two slots alternate between the
+// encode and decode calls of a ctx; see EncodeParams)
+__device__ __forceinline__ void dec_clear_next_slot(const DecodeParams& P) {
+    if (blockIdx.x == 0 && P.replay_clear) {
+#pragma unroll
+        for (int i = 0; i < 2 * kCountSpread / kBlock; i++) P.replay_clear[i * kBlock + threadIdx.x] = 0u;
     }
 }
 
@@ -361,9 +442,10 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * DecGeom<D>::CPW;
     int4 v[8];
     dec_load_tile<D>(P, cube0, lane, v);
+    dec_clear_next_slot(P);
     dec_stage_tile<D>(wl, lane, v);
     wave_lds_sync();
-    decode_tile<D, PG>(P, wl, lane, cube0, [] {});
+    decode_tile<D, PG>(P, wl, lane, cube0, [] {}, ReloadCubes<D>{P.in});
 }
 
 }  // namespace dct3d

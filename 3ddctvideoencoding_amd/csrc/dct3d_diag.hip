@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel_diag(DecodeParams P) 
     }
     DecodeParams Q = P;
     if (MODE == 2 && P.width != 0xFFFFFFFFu) Q.n_cubes = 0;  // all stores suppressed, compute kept
-    decode_tile<D, 1>(Q, wl, lane, cube0, [] {});
+    decode_tile<D, 1>(Q, wl, lane, cube0, [] {}, ReloadCubes<D>{P.in});
 }
 
 // =============================================================================================
@@ -316,9 +316,6 @@ int dct3d_decode_diag_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_
     if (rc || (rc = geometry(w, h, n_stacks, &n_cubes))) return rc;
     if (v.bd != 8) return DCT3D_EINVAL;  // the split exists for the 8x8x8 decode
     if (n_cubes == 0) return DCT3D_OK;
-    // counters (16 B) + a cube list the uncertified cubes of the garbage output may append to
-    char* s = (char*)scratch(v.device, 16 + (n_cubes + 1) * sizeof(uint32_t));
-    if (!s) return DCT3D_ENOMEM;
     DecodeParams P;
     memset(&P, 0, sizeof(P));
     P.in = d_q;
@@ -331,11 +328,9 @@ int dct3d_decode_diag_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
     P.stack_stride = P.plane * 8;
-    P.counters = (unsigned int*)s;
-    P.cube_list = (uint32_t*)(s + 16);
+    P.inv_coef_t = nullptr;  // no replay: mode 1 certifies nothing, mode 2 stores (and so flags) nothing
     const uint32_t per = DecGeom<8>::CPW * kWavesPerBlock;
     const uint32_t groups = (uint32_t)((n_cubes + per - 1) / per);
-    if (hipMemsetAsync(s, 0, 16, v.stream) != hipSuccess) return DCT3D_EDEVICE;
     if (mode == 1) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, v.stream, P);
     else hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, v.stream, P);
     return hipGetLastError() == hipSuccess ? DCT3D_OK : DCT3D_EKERNEL;

@@ -73,27 +73,10 @@ struct DecodeParams {
     uint32_t cube_base;        // decode_eg_kernel: first cube of this launch (a chunk of whole stacks)
     uint64_t plane, stack_stride;
     double dec_G, dec_E;
-    unsigned long long* flag_list;
-    unsigned int* counters;
-    uint32_t flag_cap;
-    uint32_t* cube_list;
-};
-
-struct DecodeFixupParams {
-    const int32_t* in;
-    uint8_t* out;
-    uint32_t cubes_per_stack, nbx, width;
-    uint64_t plane, stack_stride;
-    const unsigned long long* flag_list;
-    const unsigned int* counters;
-    uint32_t flag_cap;
-    const uint32_t* cube_list;
-    const double* inv_coef_t;  // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
-    // in == nullptr (fused stream decode): a replayed cube's values are re-parsed from the stream
-    const uint32_t* words;
-    uint64_t n_words;
-    const uint64_t* mark;      // bit position of every 32nd value (EgDecParams::mark)
-    const uint16_t* diag;
+    // uncertified cubes are replayed whole inside the wave (exact Java InverseDCT fold)
+    const double* inv_coef_t;    // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
+    unsigned int* replay_count;  // this call's counter slot: [0, S) cubes replayed (S = kCountSpread), or nullptr
+    unsigned int* replay_clear;  // the other slot (2S words): zeroed by block 0 for the next call
 };
 
 struct Fwd64Params {
@@ -178,6 +161,5 @@ int launch_eg_mark(const EgDecParams& P, hipStream_t st);
 int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st);
 // fused stream -> raster decode: values parsed at the marks straight into the decode's LDS staging
 int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st);
-int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st);
 
 }  // namespace dct3d

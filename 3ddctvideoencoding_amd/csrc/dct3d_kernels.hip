@@ -383,6 +383,30 @@ int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n
 // l parses the 32 values from mark m0 + l into registers, the region then receives them at their
 // diagonal positions in the decode's staging layout (face-padded cube-major), and decode_tile runs as
 // in decode_kernel.  No int32 cube-major array is written or read.
+// The rare exact replay re-parses its cube from the stream at the cube's marks (lanes 0 .. CS/32 - 1,
+// 32 values each, global reads: the wave's window is gone by then).
+template <int D>
+struct ReloadStream {
+    const uint32_t* words;
+    uint64_t n_words;
+    const uint64_t* mark;
+    const uint16_t* diag;  // the block's LDS copy
+    __device__ __forceinline__ void operator()(uint32_t g, double* cf, int lane) const {
+        constexpr int PARTS = 64 * D / 32;
+        if (lane < PARTS) {
+            BitReader<GlobalBits> r{GlobalBits{words, n_words}, 0, 0, 0, 0};
+            r.seek(mark[(uint64_t)g * PARTS + lane]);
+            for (int i = 0; i < 32; i++) {
+                uint32_t code = 1u;
+                (void)r.get(code);
+                const int k = diag[lane * 32 + i];
+                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
+                cf[k] = (double)eg_value(code) * (double)max(1, 5 * (kx + ky + kz));
+            }
+        }
+    }
+};
+
 template <int D>
 __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, EgDecParams E) {
     using G = DecGeom<D>;
@@ -390,6 +414,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     static_assert(CPW * CS == 2048 && PARTS * CPW == 64, "one wave = 64 marks");
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];
+    dec_clear_next_slot(P);
     if (E.status[2] != 0) return;  // corrupt / short stream: reported by the mark pass (block-uniform)
     {  // both loads in flight before the LDS writes
         static_assert(CS % kBlock == 0, "whole passes");
@@ -448,81 +473,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         }
     }
     wave_lds_sync();
-    decode_tile<D, 1>(P, wl, lane, cube0, [] {});
-}
-
-// Exact Java InverseDCT fold (InverseDCT.java:56-66: k ascending, zero coefficients skipped, then
-// clamp and truncation) for uncertified pixels.
-//   per-pixel entries (flag list; the 8-lanes-per-cube decode variant): one thread per entry;
-//   whole-cube entries (cube list): one block per cube, its dequantised coefficients in LDS (the
-//   zero test is block-uniform), thread t folds pixels t and t + 256 with coalesced table reads.
-__device__ __forceinline__ void store_decoded(const DecodeFixupParams& P, uint32_t g, int n, double acc) {
-    const double mn = acc < 255.0 ? acc : 255.0;
-    const double v = mn > 0.0 ? mn : 0.0;
-    const uint32_t s = g / P.cubes_per_stack;
-    const uint32_t r = g - s * P.cubes_per_stack;
-    const uint32_t by = r / P.nbx, bx = r - by * P.nbx;
-    const int z = n / 64, y = (n / 8) & 7, x = n & 7;
-    P.out[(size_t)s * P.stack_stride + (size_t)z * P.plane + (size_t)(by * 8 + y) * P.width + bx * 8 + x] =
-        (uint8_t)(int)v;
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void decode_fixup_kernel(DecodeFixupParams P) {
-    constexpr int CS = 64 * D;
-    __shared__ double cf[CS];
-    const uint32_t nf = min(P.counters[0], P.flag_cap);
-    const uint32_t ncube = P.counters[1];
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < nf; e += gridDim.x * blockDim.x) {
-        const unsigned long long v = P.flag_list[e];
-        const uint32_t g = (uint32_t)(v / CS);
-        const int n = (int)(v % CS);
-        const int32_t* q = P.in + (size_t)g * CS;
-        double acc = 0.0;
-        for (int k = 0; k < CS; k++) {
-            const int32_t qk = q[k];
-            if (qk != 0) {
-                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-                const double c = (double)qk * (double)max(1, 5 * (kx + ky + kz));
-                acc = __dadd_rn(acc, __dmul_rn(c, P.inv_coef_t[(size_t)k * CS + n]));  // InverseDCT.java:64
-            }
-        }
-        store_decoded(P, g, n, acc);
-    }
-    for (uint32_t ci = blockIdx.x; ci < ncube; ci += gridDim.x) {
-        const uint32_t g = P.cube_list[ci];
-        __syncthreads();
-        if (P.in) {
-            for (int k = threadIdx.x; k < CS; k += blockDim.x) {
-                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-                cf[k] = (double)P.in[(size_t)g * CS + k] * (double)max(1, 5 * (kx + ky + kz));
-            }
-        } else if (threadIdx.x < CS / 32) {  // fused stream decode: re-parse the cube at its marks
-            BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0};
-            r.seek(P.mark[(uint64_t)g * (CS / 32) + threadIdx.x]);
-            for (int i = 0; i < 32; i++) {
-                uint32_t code = 1u;
-                (void)r.get(code);
-                const int k = P.diag[threadIdx.x * 32 + i];
-                const int kz = k / 64, ky = (k / 8) & 7, kx = k & 7;
-                cf[k] = (double)eg_value(code) * (double)max(1, 5 * (kx + ky + kz));
-            }
-        }
-        __syncthreads();
-        double acc[CS / 256];
-#pragma unroll
-        for (int i = 0; i < CS / 256; i++) acc[i] = 0.0;
-        for (int k = 0; k < CS; k++) {
-            const double c = cf[k];
-            if (c != 0.0) {
-#pragma unroll
-                for (int i = 0; i < CS / 256; i++)
-                    acc[i] = __dadd_rn(acc[i], __dmul_rn(c, P.inv_coef_t[(size_t)k * CS + threadIdx.x + 256 * i]));
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < CS / 256; i++) store_decoded(P, g, threadIdx.x + 256 * i, acc[i]);
-    }
+    decode_tile<D, 1>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, s_diag});
 }
 
 // =============================================================================================
@@ -591,10 +542,5 @@ int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStre
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_decode_fixup(int D, const DecodeFixupParams& P, int grid, hipStream_t st) {
-    if (D == 8) hipLaunchKernelGGL(decode_fixup_kernel<8>, dim3(grid), dim3(256), 0, st, P);
-    else hipLaunchKernelGGL(decode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
 
 }  // namespace dct3d

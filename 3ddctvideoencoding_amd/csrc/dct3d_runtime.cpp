@@ -79,6 +79,7 @@ struct dct3d_ctx {
     DevBuf d_enc_counts;
     int enc_slot = 0;
     int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
+    bool last_count_decode = false;  // the slot holds a decode's whole-cube replays
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
@@ -357,6 +358,10 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
             st->n_flagged += w[i];
             st->n_rechecked += w[kCountSpread + i];
         }
+        if (c->last_count_decode) {  // decode: every replay is a whole cube
+            st->n_overflow_cubes = st->n_flagged;
+            st->n_flagged *= (uint64_t)c->plan.cs;
+        }
         return DCT3D_OK;
     } else if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
         return DCT3D_EDEVICE;
@@ -391,6 +396,19 @@ static int ensure_flag_buffers(dct3d_ctx* c, uint64_t n_cubes) {
     if (rc) return rc;
     c->flag_cap = (uint32_t)cap;
     return DCT3D_OK;
+}
+
+// Decode: uncertified cubes are replayed inside the wave; the replay count goes to the ctx's current
+// counter slot, and the launch zeroes the other one for the next call (see d_enc_counts).
+static void set_dec_replay(dct3d_ctx* c, DecodeParams& P) {
+    P.inv_coef_t = (const double*)c->d_inv_coef.p;
+    P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
+    P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+}
+static void end_dec_replay(dct3d_ctx* c) {
+    c->last_count_slot = c->enc_slot;
+    c->last_count_decode = true;
+    c->enc_slot ^= 1;
 }
 
 static int forward_f64_raster(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, uint64_t n_cubes, double* d_out) {
@@ -465,6 +483,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
             (void)hipEventRecord(ev[3], c->stream);
         }
         c->last_count_slot = c->enc_slot;
+        c->last_count_decode = false;
         c->enc_slot ^= 1;
         c->last_units = n_cubes * (uint64_t)c->plan.cs;
         c->last_valid = true;
@@ -504,11 +523,8 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     c->last_valid = false;
     c->last_count_slot = -1;
     if (n_cubes == 0) return DCT3D_OK;
-    rc = ensure_flag_buffers(c, n_cubes);
-    if (rc) return rc;
     const int D = c->bd;
     const uint64_t plane = (uint64_t)w * h;
-    if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     DecodeParams P;
     P.in = d_q;
     P.out = d_raster;
@@ -525,34 +541,16 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     // test option: widen the certification margin so that most pixels are uncertified and their cubes
     // take the whole-cube replay path (tests/test_gpu_parity.py); a wider margin is never unsafe
     P.dec_E += c->opt_dec_margin;
-    P.flag_list = (unsigned long long*)c->d_flags.p;
-    P.counters = (unsigned int*)c->d_counters.p;
-    P.flag_cap = c->flag_cap;
-    P.cube_list = (uint32_t*)c->d_cubes.p;
+    set_dec_replay(c, P);
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (launch_decode(D, P, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
-    DecodeFixupParams F;
-    F.in = d_q;
-    F.out = d_raster;
-    F.cubes_per_stack = P.cubes_per_stack;
-    F.nbx = P.nbx;
-    F.width = P.width;
-    F.plane = P.plane;
-    F.stack_stride = P.stack_stride;
-    F.flag_list = P.flag_list;
-    F.counters = P.counters;
-    F.flag_cap = P.flag_cap;
-    F.cube_list = P.cube_list;
-    F.inv_coef_t = (const double*)c->d_inv_coef.p;
-    F.words = nullptr;
-    F.n_words = 0;
-    F.mark = nullptr;
-    F.diag = nullptr;
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_decode_fixup(D, F, 256, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    if (ev) {  // one launch: the second event pair brackets nothing
+        (void)hipEventRecord(ev[1], c->stream);
+        (void)hipEventRecord(ev[2], c->stream);
+        (void)hipEventRecord(ev[3], c->stream);
+    }
+    end_dec_replay(c);
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = true;
     return DCT3D_OK;
@@ -1054,7 +1052,6 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     const uint64_t plane = (uint64_t)w * h;
     const uint64_t cps = (uint64_t)(w / 8) * (h / 8);
     uint8_t* out = out_stack0 - (size_t)st0 * plane * D;  // rebased: stack st0 at out_stack0
-    if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     DecodeParams P;
     P.in = nullptr;
     P.out = out;
@@ -1069,34 +1066,15 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
     P.dec_E += c->opt_dec_margin;  // test option (see above)
-    P.flag_list = (unsigned long long*)c->d_flags.p;
-    P.counters = (unsigned int*)c->d_counters.p;
-    P.flag_cap = c->flag_cap;
-    P.cube_list = (uint32_t*)c->d_cubes.p;
+    set_dec_replay(c, P);
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (launch_decode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
-    DecodeFixupParams F;
-    F.in = nullptr;
-    F.out = out;
-    F.cubes_per_stack = P.cubes_per_stack;
-    F.nbx = P.nbx;
-    F.width = P.width;
-    F.plane = P.plane;
-    F.stack_stride = P.stack_stride;
-    F.flag_list = P.flag_list;
-    F.counters = P.counters;
-    F.flag_cap = P.flag_cap;
-    F.cube_list = P.cube_list;
-    F.inv_coef_t = (const double*)c->d_inv_coef.p;
-    F.words = E.words;
-    F.n_words = E.n_words;
-    F.mark = E.mark;
-    F.diag = E.diag;
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_decode_fixup(D, F, 256, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    if (ev) {
+        (void)hipEventRecord(ev[1], c->stream);
+        (void)hipEventRecord(ev[2], c->stream);
+        (void)hipEventRecord(ev[3], c->stream);
+    }
     return DCT3D_OK;
 }
 extern "C" {
@@ -1117,8 +1095,8 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
     EgDecParams E;
     if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
-    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
     if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
+    end_dec_replay(c);
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = true;
     return eg_decode_status(c, E, end_bit);
@@ -1138,13 +1116,13 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     EgDecParams E;
     if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E))) return rc;
-    if ((rc = ensure_flag_buffers(c, n_cubes))) return rc;
     // the raster leaves in chunks of stacks while the next chunk decodes (the stream is small: no upload)
     const size_t px = n_cubes * c->plan.cs / n_stacks;
     rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
         return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
     });
     if (rc) return rc;
+    end_dec_replay(c);
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = true;
     return eg_decode_status(c, E, end_bit);
