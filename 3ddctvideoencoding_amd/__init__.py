@@ -56,7 +56,8 @@ class Dct3dError(RuntimeError):
 class PlanInfo(C.Structure):
     _fields_ = [("cube_size", C.c_int), ("n_mults", C.c_int), ("treeified", C.c_int), ("coef_dc", C.c_double),
                 ("dec_G", C.c_double), ("dec_E", C.c_double), ("enc_rstep", C.c_float * 32),
-                ("enc_G", C.c_float * 32), ("enc_E", C.c_float * 32), ("enc_thr64", C.c_double * 32)]
+                ("enc_G", C.c_float * 32), ("enc_E", C.c_float * 32), ("enc_thr64", C.c_double * 32),
+                ("dec_l1_max", C.c_float)]
 
 
 class Stats(C.Structure):
@@ -176,7 +177,7 @@ def plan_query(block_w: int = 8, block_h: int = 8, block_d: int = 8) -> dict:
     _check(lib().dct3d_plan_query(block_w, block_h, block_d, C.byref(info), _ptr(ng), _ptr(coef), _ptr(gof), _ptr(K)),
            "dct3d_plan_query")
     return {"cube_size": info.cube_size, "n_mults": info.n_mults, "treeified": bool(info.treeified),
-            "coef_dc": info.coef_dc, "dec_G": info.dec_G, "dec_E": info.dec_E,
+            "coef_dc": info.coef_dc, "dec_G": info.dec_G, "dec_E": info.dec_E, "dec_l1_max": info.dec_l1_max,
             "enc_rstep": np.array(info.enc_rstep[:]), "enc_G": np.array(info.enc_G[:]),
             "enc_E": np.array(info.enc_E[:]), "enc_thr64": np.array(info.enc_thr64[:]), "ngroups": ng, "coef": coef.reshape(cs, 64),
             "group_of": gof.reshape(cs, cs), "enc_K": K}

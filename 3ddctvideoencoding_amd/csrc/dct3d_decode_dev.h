@@ -63,13 +63,6 @@ __device__ __forceinline__ uint32_t cvt_u32_sat(double v) {
 // (0x413: the biased exponent of 2^20; 2^19: the offset 0.5 * 2^20).
 constexpr double kFixMagic = 1572864.0;  // 1.5 * 2^20
 constexpr uint32_t kFixHi = 0x41380000u;
-// max(0, hi - kFixHi): max(0, floor(v)) in one VALU op (unsigned subtract, clamped at 0)
-__device__ __forceinline__ uint32_t fix_floor0(uint32_t hi) {
-    uint32_t t;
-    asm("v_sub_u32_e64 %0, %1, %2 clamp" : "=v"(t) : "v"(hi), "s"(kFixHi));
-    return t;
-}
-
 // staged input of one tile (CPW cubes, 8 KiB): 8 coalesced 1 KiB loads per wave
 // (4-byte values: int32 quantised cubes, or the float cubes of the drop-in kernels)
 template <int D>
@@ -180,23 +173,43 @@ struct ReloadCubes {  // from the int32 cube-major input
 template <int D, class Reload>
 __device__ __attribute__((noinline)) const uint8_t* decode_replay_cube(const double* inv_coef_t, Reload reload,
                                                                        char* wl, int lane, uint32_t g) {
-    constexpr int CS = 64 * D, NP = CS / 64;
-    static_assert(CS * 8 + CS <= kDecWaveLds, "replay scratch fits the wave's region");
+    constexpr int CS = 64 * D, NP = CS / 64, U = 16 / NP;  // 16 table loads in flight per round
+    static_assert(CS * 8 + CS * 2 + CS <= kDecWaveLds, "replay scratch fits the wave's region");
     double* cf = (double*)wl;
-    uint8_t* ob = (uint8_t*)(wl + CS * 8);
+    uint16_t* nzk = (uint16_t*)(wl + CS * 8);
+    uint8_t* ob = (uint8_t*)(wl + CS * 10);
     wave_lds_sync();
     reload(g, cf, lane);
+    wave_lds_sync();
+    // the non-zero coefficients in ascending k (the fold skips zeros: InverseDCT.java:60)
+    uint32_t nnz = 0;
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        const bool nz = cf[64 * i + lane] != 0.0;
+        const unsigned long long bm = __ballot(nz);
+        if (nz) nzk[nnz + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] = (uint16_t)(64 * i + lane);
+        nnz += (uint32_t)__builtin_popcountll(bm);
+    }
     wave_lds_sync();
     double acc[NP];
 #pragma unroll
     for (int i = 0; i < NP; i++) acc[i] = 0.0;
     const double* tab = inv_coef_t + lane;
-    for (int k = 0; k < CS; k++) {
-        const double cv = cf[k];  // the same word for every lane: a uniform branch
-        if (cv != 0.0) {
+    // U coefficients per round with all their table loads in flight; a padded slot (past nnz) multiplies
+    // by 0 and adds +-0, which leaves acc's value unchanged
+    for (uint32_t j = 0; j < nnz; j += U) {
+        double cv[U], t[U][NP];
 #pragma unroll
-            for (int i = 0; i < NP; i++) acc[i] = __dadd_rn(acc[i], __dmul_rn(cv, tab[(size_t)k * CS + 64 * i]));
+        for (int u = 0; u < U; u++) {
+            const uint32_t kk = nzk[min(j + u, nnz - 1)];
+            cv[u] = j + u < nnz ? cf[kk] : 0.0;
+#pragma unroll
+            for (int i = 0; i < NP; i++) t[u][i] = tab[(size_t)kk * CS + 64 * i];
         }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int i = 0; i < NP; i++) acc[i] = __dadd_rn(acc[i], __dmul_rn(cv[u], t[u][i]));
     }
 #pragma unroll
     for (int i = 0; i < NP; i++) {
@@ -223,58 +236,46 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     const uint32_t g = cube0 + c;
     const bool valid = g < P.n_cubes;
 
-    // ---- layout A: dequantise, amax ----
-    // cf = q * step exactly: a 24-bit integer multiply, then an exact conversion to fp64.  One integer
-    // max / min pass over q bounds everything: with M = max(q, ~q) over the lane's values other than
-    // slot (ky, e) = (0, 0), |q| <= M + 1, so |q * step| <= (M + 1) * (sb + 50) (the lane's largest
-    // step); slot (0, 0) (the DC on the DC lane, step 1) enters as its exact product t00.  Any |q| >=
-    // 2^15 (never produced by an encoder of 8-bit frames) sends the cube to the exact replay, which
-    // also keeps the 24-bit products exact.
+    // ---- layout A: dequantise, L1 ----
+    // cf = q * step in fp64: an exact conversion and an exact product (|q * step| < 2^38) for every int32
+    // q.  L1 = sum |cf| over the cube bounds both the error (|v - v_java| <= dec_G L1 + dec_E) and the
+    // values (|v| <= Bmax L1): one fp64 add per value (|x| is a source modifier), summed over the lane,
+    // then over the cube's lanes in fp32 with a final factor that covers every rounding on the way
+    // (fp64 sum 2^-48, the conversion and five fp32 roundings 6 * 2^-24 < 2^-19).
     double b[8][4];
-    float amax_f;
-    bool q_range_bad;
+    float l1_f;
     {
         const int sb = 5 * (4 * h + k);                     // step = sb + 5 (e + ky); DC (e = ky = 0): 1
-        int stp[11];
-        stp[0] = max(sb, 1);
+        double stp[11];
+        stp[0] = (double)max(sb, 1);
 #pragma unroll
-        for (int j = 1; j < 11; j++) stp[j] = sb + 5 * j;
+        for (int j = 1; j < 11; j++) stp[j] = (double)(sb + 5 * j);
         const char* src = wl + c * G::SA_C + k * G::SA_F + h * 16;
         int4 raw[8];  // all eight LDS reads in flight before the first use
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) raw[ky] = *(const int4*)(src + ky * 32);
-        int qmax = max(raw[0].y, max(raw[0].z, raw[0].w)), qmin = min(raw[0].y, min(raw[0].z, raw[0].w));
+        double l1 = 0.0;
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) {
             const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
 #pragma unroll
-            for (int e = 0; e < 4; e++) b[ky][e] = (double)__mul24(vv[e], stp[e + ky]);
-            if (ky) {
-                qmax = max(qmax, max(max(vv[0], vv[1]), max(vv[2], vv[3])));
-                qmin = min(qmin, min(min(vv[0], vv[1]), min(vv[2], vv[3])));
+            for (int e = 0; e < 4; e++) {
+                b[ky][e] = __dmul_rn((double)vv[e], stp[e + ky]);
+                l1 = __dadd_rn(l1, __builtin_fabs(b[ky][e]));
             }
         }
-        const int q00 = raw[0].x;
-        const int mq = max(qmax, ~qmin);      // >= |q| - 1 over the 31 values
-        const int m00 = max(q00, ~q00);       // >= |q00| - 1
-        q_range_bad = max(mq, m00) >= 0x8000;
-        const int t00 = __mul24(q00, stp[0]);
-        const uint32_t amax_i = max((uint32_t)max(t00, -t00), __umul24((uint32_t)mq + 1u, (uint32_t)(sb + 50)));
-        // float upper bound of amax (nearest rounding is within 2^-24 relative; the product with
-        // 1 + 2^-22 rounds to at least amax): the cube reduction then moves one dword per step
-        amax_f = (float)amax_i * (1.0f + 0x1p-22f);
+        l1_f = (float)l1;
     }
     after_a();
-    // amax over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
-    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0xB1, 0xF, 0xF, false)));  // quad_perm xor 1
-    amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x4E, 0xF, 0xF, false)));  // quad_perm xor 2
+    // L1 over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
+    l1_f += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, l1_f), 0xB1, 0xF, 0xF, false));  // quad_perm xor 1
+    l1_f += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, l1_f), 0x4E, 0xF, 0xF, false));  // quad_perm xor 2
     if constexpr (D == 8)
-        amax_f = fmaxf(amax_f, __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, amax_f), 0x141, 0xF, 0xF, false)));  // row_half_mirror
+        l1_f += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, l1_f), 0x141, 0xF, 0xF, false));  // row_half_mirror
     {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, amax_f), __builtin_bit_cast(uint32_t, amax_f), false, false);
-        amax_f = fmaxf(__builtin_bit_cast(float, (uint32_t)sw[0]), __builtin_bit_cast(float, (uint32_t)sw[1]));
+        const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, l1_f), __builtin_bit_cast(uint32_t, l1_f), false, false);
+        l1_f = (__builtin_bit_cast(float, (uint32_t)sw[0]) + __builtin_bit_cast(float, (uint32_t)sw[1])) * (1.0f + 0x1p-19f);
     }
-    const double amax = (double)amax_f;
 
     // ---- inverse pass Y ----
     constexpr int G1 = PG == 0 ? 4 : PG;
@@ -349,41 +350,39 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     }
 
     // ---- certify, clamp + truncate, store ----
-    // |v - v_java| <= m (dct3d_plan.cpp).  The byte is min(max(0, floor(v)), 255), monotone in v, so it
-    // is Java's byte when floor is constant over [v - m, v + m]: frac(v) >= m and frac(v) + m < 1.  In
-    // the fixed-point view (kFixMagic, |v| < 2^19) lo = frac(v) 2^32 to within 1/2 unit, so with
-    // mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] for every pixel proves it: the lane keeps
-    // min and max of lo (one v_min3 / v_max3 per two pixels) and tests them once.
-    // Range: |v| <= amax * sum_k |c(n, k)| <= 18.4 amax (8^1.5 bounds the sum), so amax < 2^16 gives
-    // |v| < 1.21e6 < 1.5 * 2^20 = kFixMagic: w = v + kFixMagic > 0.  For |v| >= 2^19 the view is not
-    // fixed point, but the byte still is Java's: w >= 2^21 has a high word above kFixHi + 255 (-> 255,
-    // and v_java > 2^19 - m > 255), w < 2^20 one below kFixHi (-> 0, and v_java < 0), whatever the
-    // certificate then says.  amax >= 2^16 (never from an encoder of 8-bit frames) goes to the replay.
-    const double m = __builtin_fmin(amax * P.dec_G + P.dec_E, 0.5);
+    // |v - v_java| <= m = dec_G L1 + dec_E (dct3d_plan.cpp).  The byte is clamp(floor(v), 0, 255),
+    // monotone in v, so it is Java's byte when floor is constant over [v - m, v + m]: frac(v) >= m and
+    // frac(v) + m < 1.  Fixed-point view (kFixMagic, |v| < 2^19): the low word lo = frac(v) 2^32 to within
+    // 1/2 unit, so with mi = m 2^32 + 1/2 rounded up, lo in [mi, 2^32 - 1 - mi] for every pixel proves it
+    // (the lane keeps min and max of lo: one v_min3 / v_max3 per two pixels).  The high word is
+    // kFixHi + floor(v), and its low half floor(v) as a signed 16-bit value while |v| < 2^15, which
+    // L1 < dec_l1_max guarantees (|v| <= Bmax L1 + m); v_sat_pk_u8_i16 then clamps two pixels to bytes
+    // in one op.  A cube with a larger L1 (never from an encoder of 8-bit frames) goes to the replay.
+    const double m = __builtin_fmin((double)l1_f * P.dec_G + P.dec_E, 0.5);
     const uint32_t mi = (uint32_t)__builtin_ceil(__fma_rn(m, 0x1p32, 0.5)) + 1u;  // + 1: m's own rounding
     const int y = (D == 8) ? k : (4 * h + k);
     const int x0 = (D == 8) ? 4 * h : 0;
-    bool flag = q_range_bad | (amax_f >= 65536.0f);
+    bool flag = !(l1_f < P.dec_l1_max);
     uint32_t lo_min = 0xFFFFFFFFu, lo_max = 0u;
     uint32_t outw[D][NXC / 4];
-    const uint32_t c255 = 255u;
 #pragma unroll
     for (int z = 0; z < D; z++) {
 #pragma unroll
         for (int wd = 0; wd < NXC / 4; wd++) {
-            uint32_t w = 0;
+            uint32_t hw[4];
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const uint64_t fx = __builtin_bit_cast(uint64_t, __dadd_rn(cz[z][4 * wd + e], kFixMagic));
-                const uint32_t tl = fix_floor0((uint32_t)(fx >> 32));
+                hw[e] = (uint32_t)(fx >> 32);
                 lo_min = min(lo_min, (uint32_t)fx);
                 lo_max = max(lo_max, (uint32_t)fx);
-                // byte e of w = min(tl, 255) (SDWA byte insert: the other bytes are preserved)
-                if (e == 0) w = min(tl, 255u);
-                else if (e == 1) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
-                else if (e == 2) asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
-                else asm("v_min_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(w) : "v"(tl), "v"(c255));
             }
+            // bytes 0..3 = clamp(floor(v_e), 0, 255): pairs of signed 16-bit floors, saturated to u8
+            const uint32_t p01 = __builtin_amdgcn_perm(hw[1], hw[0], 0x05040100u);
+            const uint32_t p23 = __builtin_amdgcn_perm(hw[3], hw[2], 0x05040100u);
+            uint32_t w;
+            asm("v_sat_pk_u8_i16_e32 %0, %1" : "=v"(w) : "v"(p01));
+            asm("v_sat_pk_u8_i16_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD" : "+v"(w) : "v"(p23));
             asm volatile("" : "+v"(w));  // one output word at a time (bounded live range)
             outw[z][wd] = w;
         }

@@ -72,7 +72,8 @@ struct DecodeParams {
     FastDiv div_cps, div_nbx;
     uint32_t cube_base;        // decode_eg_kernel: first cube of this launch (a chunk of whole stacks)
     uint64_t plane, stack_stride;
-    double dec_G, dec_E;
+    double dec_G, dec_E;       // certificate: margin = dec_G * sum |dequantised| + dec_E
+    float dec_l1_max;          // sum |dequantised| >= this: the cube goes to the exact replay
     // uncertified cubes are replayed whole inside the wave (exact Java InverseDCT fold)
     const double* inv_coef_t;    // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
     unsigned int* replay_count;  // this call's counter slot: [0, S) cubes replayed (S = kCountSpread), or nullptr

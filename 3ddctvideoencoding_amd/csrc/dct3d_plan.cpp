@@ -26,8 +26,9 @@ namespace dct3d {
 // Tracked value (error analysis)
 // =============================================================================================
 struct Tracked {
-    std::vector<double> w;  // exact linear functional over the cube's inputs
-    double e = 0.0;         // rounding-error bound for inputs with |x_n| <= 1
+    std::vector<double> w;   // exact linear functional over the cube's inputs
+    double e = 0.0;          // rounding-error bound for inputs with |x_n| <= 1
+    std::vector<double> ev;  // (decoder analysis) per-input error coefficients: error <= sum_n ev[n] |x_n|
     Tracked() = default;
     explicit Tracked(size_t n) : w(n, 0.0) {}
 };
@@ -35,6 +36,7 @@ struct Tracked {
 namespace {
 double g_u = 0.0;     // unit roundoff of the analysed arithmetic
 bool g_f32 = true;    // constants rounded to float (else double)
+bool g_ev = false;    // track the per-input error coefficients (Tracked::ev)
 double l1(const std::vector<double>& w) {
     double s = 0;
     for (double x : w) s += std::fabs(x);
@@ -43,44 +45,59 @@ double l1(const std::vector<double>& w) {
 double crep(double c) { return g_f32 ? (double)(float)c : c; }
 // |stored constant - true constant|: rounding to T plus the double literal's own error
 double cerr(double c) { return std::fabs(crep(c) - c) + std::ldexp(std::fabs(c), -53); }
+// one rounding of the result: |rounded - exact| <= u |exact| <= u (sum |w_n x_n| + error), i.e. per
+// input n: u (|w_n| + ev_n)
 void round_term(Tracked& r, bool exact) {
-    if (!exact) r.e += g_u * (l1(r.w) + r.e);
+    if (exact) return;
+    r.e += g_u * (l1(r.w) + r.e);
+    for (size_t i = 0; i < r.ev.size(); i++) r.ev[i] += g_u * (std::fabs(r.w[i]) + r.ev[i]);
+}
+Tracked make_like(const Tracked& a) {
+    Tracked r(a.w.size());
+    if (g_ev) r.ev.assign(a.w.size(), 0.0);
+    return r;
 }
 }  // namespace
 
 template <bool EX = false>
 inline Tracked dadd(const Tracked& a, const Tracked& b) {
-    Tracked r(a.w.size());
+    Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = a.w[i] + b.w[i];
+    for (size_t i = 0; i < r.ev.size(); i++) r.ev[i] = a.ev[i] + b.ev[i];
     r.e = a.e + b.e;
     round_term(r, EX);
     return r;
 }
 template <bool EX = false>
 inline Tracked dsub(const Tracked& a, const Tracked& b) {
-    Tracked r(a.w.size());
+    Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = a.w[i] - b.w[i];
+    for (size_t i = 0; i < r.ev.size(); i++) r.ev[i] = a.ev[i] + b.ev[i];
     r.e = a.e + b.e;
     round_term(r, EX);
     return r;
 }
 inline Tracked dmulc(double c, const Tracked& a) {
-    Tracked r(a.w.size());
+    Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = c * a.w[i];
+    for (size_t i = 0; i < r.ev.size(); i++) r.ev[i] = std::fabs(crep(c)) * a.ev[i] + cerr(c) * std::fabs(a.w[i]);
     r.e = std::fabs(crep(c)) * a.e + cerr(c) * l1(a.w);
     round_term(r, false);
     return r;
 }
 inline Tracked dfmac(double c, const Tracked& a, const Tracked& b) {
-    Tracked r(a.w.size());
+    Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = c * a.w[i] + b.w[i];
+    for (size_t i = 0; i < r.ev.size(); i++)
+        r.ev[i] = std::fabs(crep(c)) * a.ev[i] + cerr(c) * std::fabs(a.w[i]) + b.ev[i];
     r.e = std::fabs(crep(c)) * a.e + cerr(c) * l1(a.w) + b.e;
     round_term(r, false);
     return r;
 }
 inline Tracked dhalf(const Tracked& a) {
-    Tracked r(a.w.size());
+    Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = 0.5 * a.w[i];
+    for (size_t i = 0; i < r.ev.size(); i++) r.ev[i] = 0.5 * a.ev[i];
     r.e = 0.5 * a.e;
     return r;
 }
@@ -266,14 +283,19 @@ void analyse_encoder(Plan& p) {
 }
 
 // Decoder: kernel order = inverse pass Y (face layout) -> inverse pass X -> inverse pass Z, fp64.
-void analyse_decoder(Plan& p, std::vector<double>& K, std::vector<double>& L1) {
+// Returns, per output n: K[n] = error bound for unit inputs (sum_i ev[n][i]), L1[n] = sum_i |w[n][i]|,
+// and G1 = max over n, i of ev[n][i] + J |w[n][i]| (J: the Java fold's own error per unit term), the
+// error per unit of sum_i |x_i|; Bmax = max |w[n][i]| (|v_n| <= Bmax sum_i |x_i|).
+void analyse_decoder(Plan& p, std::vector<double>& K, std::vector<double>& L1, double J, double& G1, double& Bmax) {
     const int D = p.cd, cs = p.cs;
     g_u = std::ldexp(1.0, -53);
     g_f32 = false;
+    g_ev = true;
     std::vector<Tracked> v(cs);
     for (int n = 0; n < cs; n++) {
         v[n] = Tracked(cs);
         v[n].w[n] = 1.0;
+        v[n].ev.assign(cs, 0.0);
     }
     auto at = [&](int z, int y, int x) -> Tracked& { return v[(z * 8 + y) * 8 + x]; };
     for (int z = 0; z < D; z++)
@@ -304,11 +326,18 @@ void analyse_decoder(Plan& p, std::vector<double>& K, std::vector<double>& L1) {
                 for (int z = 0; z < 4; z++) at(z, y, x) = r[z];
             }
         }
+    g_ev = false;
     K.assign(cs, 0.0);
     L1.assign(cs, 0.0);
+    G1 = 0.0;
+    Bmax = 0.0;
     for (int n = 0; n < cs; n++) {
         K[n] = v[n].e;
         L1[n] = l1(v[n].w);
+        for (int i = 0; i < cs; i++) {
+            G1 = std::max(G1, v[n].ev[i] + J * std::fabs(v[n].w[i]));
+            Bmax = std::max(Bmax, std::fabs(v[n].w[i]));
+        }
     }
 }
 
@@ -478,12 +507,21 @@ bool build_plan(int cw, int ch, int cd, Plan& p) {
     }
 
     // ---- decoder certification (fp64 kernel vs the Java fold) ----
+    // Java's fold (InverseDCT.java:56-66) of at most cs products, each rounded, its coefficients within
+    // a few ulps of the exact basis: |v_java - v_exact| <= J sum_k |x_k B_nk| with J = (cs + 16) 2^-52.
+    // The kernel: |v_gpu - v_exact| <= sum_k ev[n][k] |x_k| (analyse_decoder).  So with
+    // L1x = sum_k |x_k| (the kernel's upper bound of it), |v_gpu - v_java| <= G1 L1x (+ dec_E).
     std::vector<double> Kd, L1d;
-    analyse_decoder(p, Kd, L1d);
+    double G1 = 0.0, Bmax = 0.0;
+    const double J = (cs + 16) * std::ldexp(1.0, -52);
+    analyse_decoder(p, Kd, L1d, J, G1, Bmax);
     double gd = 0.0;
-    for (int n = 0; n < cs; n++) gd = std::max(gd, Kd[n] + (cs + 16) * std::ldexp(L1d[n], -52));
-    p.dec_G = gd * (1.0 + 1e-3);
+    for (int n = 0; n < cs; n++) gd = std::max(gd, Kd[n] + J * L1d[n]);
+    p.dec_G = G1 * (1.0 + 1e-3);
     p.dec_E = 1e-12;
+    // the kernel's byte packing reads floor(v) as a signed 16-bit value: |v| <= Bmax L1x must stay below
+    // 2^15 - 1 (with room for the error terms)
+    p.dec_l1_max = (float)(32000.0 / Bmax);
     p.fwd64_K = gd;
     return true;
 }

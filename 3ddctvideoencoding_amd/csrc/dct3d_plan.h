@@ -41,8 +41,10 @@ struct Plan {
     double enc_thr64[kMaxS] = {};         // 0.5 - 2 * max_k E64_k per s (bound derivation: dct3d_plan.cpp)
 
     // ---- fused-decode certification (fp64 kernel) ----
-    // |v_fp64 - v_java| <= A_in * dec_G + dec_E, A_in = max |dequantised coefficient| in the cube.
+    // |v_fp64 - v_java| <= L1_in * dec_G + dec_E, L1_in = sum |dequantised coefficient| over the cube;
+    // a cube with L1_in >= dec_l1_max (|v| could reach 2^15) goes to the exact replay.
     double dec_G = 0.0, dec_E = 0.0;
+    float dec_l1_max = 0.0f;
 
     // ---- inverse fp32-output / forward fp64-output kernels: informational bounds ----
     double fwd64_K = 0.0;                 // fp64 forward error per unit input magnitude

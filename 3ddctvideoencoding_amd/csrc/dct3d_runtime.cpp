@@ -158,6 +158,7 @@ int dct3d_plan_query(int bw, int bh, int bd, dct3d_plan_info* info, int32_t* ngr
         info->coef_dc = p.coef_dc;
         info->dec_G = p.dec_G;
         info->dec_E = p.dec_E;
+        info->dec_l1_max = p.dec_l1_max;
         memcpy(info->enc_rstep, p.enc_rstep, sizeof(info->enc_rstep));
         memcpy(info->enc_G, p.enc_G, sizeof(info->enc_G));
         memcpy(info->enc_E, p.enc_E, sizeof(info->enc_E));
@@ -538,6 +539,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     P.stack_stride = plane * D;
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
+    P.dec_l1_max = c->plan.dec_l1_max;
     // test option: widen the certification margin so that most pixels are uncertified and their cubes
     // take the whole-cube replay path (tests/test_gpu_parity.py); a wider margin is never unsafe
     P.dec_E += c->opt_dec_margin;
@@ -1065,6 +1067,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     P.stack_stride = plane * D;
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
+    P.dec_l1_max = c->plan.dec_l1_max;
     P.dec_E += c->opt_dec_margin;  // test option (see above)
     set_dec_replay(c, P);
     hipEvent_t* ev = timing_slot(c);

@@ -60,7 +60,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written past its end) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 6
+#define DCT3D_ABI_VERSION 7
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -68,7 +68,8 @@ typedef struct dct3d_ctx dct3d_ctx;
 typedef struct {
     uint64_t n_units;          /* coefficients (encode) or pixels (decode) produced by the last call */
     uint64_t n_flagged;        /* units of the last call re-done by the exact Java fold */
-    uint64_t n_overflow_cubes; /* cubes of the last call fully re-done because the flag list was full */
+    uint64_t n_overflow_cubes; /* cubes of the last call re-done whole by the exact fold (decode: every
+                                  replay; 8x8x4 encode: the flag list was full) */
     /* HIP-event timing of every encode/decode call since dct3d_reset_timers (profiling on) */
     uint64_t n_timed;          /* calls timed */
     double kernel_ms_total;    /* main transform kernel, summed */
@@ -83,11 +84,12 @@ typedef struct {
     int n_mults;          /* sum over coefficients of Java multiplication groups (11,567 for 8^3) */
     int treeified;        /* 1 if Java's HashMap would have treeified a bin (fold order then unverified) */
     double coef_dc;       /* the single DC group coefficient (DCT.java:110 with k = 0) */
-    double dec_G, dec_E;  /* decode certification: margin = max|coef| * dec_G + dec_E */
+    double dec_G, dec_E;  /* decode certification: margin = L1 * dec_G + dec_E, L1 = sum |q * step| of the cube */
     float enc_rstep[32];  /* encode certification per s = kx+ky+kz: fp32(1/max(1,5s)) */
     float enc_G[32];      /*   threshold_s = 0.5 - (A * G_s + E_s), A = max|x - mean| of the cube */
     float enc_E[32];
     double enc_thr64[32]; /* 8x8x8 second certificate: settled iff |q64 - rint(q64)| < enc_thr64[s] */
+    float dec_l1_max;     /* decode: a cube with L1 >= dec_l1_max takes the exact replay (|v| < 2^15) */
 } dct3d_plan_info;
 
 /* The plan for block dims (bw, bh, bd): the MI355X build's DCT.initialize (DCT.java:77-163) and
