@@ -341,7 +341,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             for (int z = 0; z < D; z++) col[i][z] = cz[z][e0 + i];
         if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
 #pragma unroll
-        for (int i = 0; i < G3; i++) idctN<D>(col[i]);
+        for (int i = 0; i < G3; i++) idctN_fix<D>(col[i], kFixMagic);  // outputs v + kFixMagic
         if (PG) for (int i = 0; i < G3; i++) pin(col[i]);
 #pragma unroll
         for (int i = 0; i < G3; i++)
@@ -372,7 +372,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             uint32_t hw[4];
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                const uint64_t fx = __builtin_bit_cast(uint64_t, __dadd_rn(cz[z][4 * wd + e], kFixMagic));
+                const uint64_t fx = __builtin_bit_cast(uint64_t, cz[z][4 * wd + e]);  // w = v + kFixMagic
                 hw[e] = (uint32_t)(fx >> 32);
                 lo_min = min(lo_min, (uint32_t)fx);
                 lo_max = max(lo_max, (uint32_t)fx);

@@ -94,6 +94,13 @@ inline Tracked dfmac(double c, const Tracked& a, const Tracked& b) {
     round_term(r, false);
     return r;
 }
+inline Tracked dneg(const Tracked& a) {
+    Tracked r = a;
+    for (double& x : r.w) x = -x;
+    return r;
+}
+// the decode's offset forms: analysed as the plain product / halving (see dct_butterfly.h idct8_fix)
+inline Tracked dfmac_k(double c, const Tracked& a, double) { return dmulc(c, a); }
 inline Tracked dhalf(const Tracked& a) {
     Tracked r = make_like(a);
     for (size_t i = 0; i < r.w.size(); i++) r.w[i] = 0.5 * a.w[i];
@@ -101,6 +108,7 @@ inline Tracked dhalf(const Tracked& a) {
     r.e = 0.5 * a.e;
     return r;
 }
+inline Tracked dhalf_k(const Tracked& a, double) { return dhalf(a); }
 
 }  // namespace dct3d
 
@@ -317,12 +325,12 @@ void analyse_decoder(Plan& p, std::vector<double>& K, std::vector<double>& L1, d
             if (D == 8) {
                 Tracked r[8];
                 for (int z = 0; z < 8; z++) r[z] = at(z, y, x);
-                idct8(r);
+                idct8_fix(r, 0.0);
                 for (int z = 0; z < 8; z++) at(z, y, x) = r[z];
             } else {
                 Tracked r[4];
                 for (int z = 0; z < 4; z++) r[z] = at(z, y, x);
-                idct4(r);
+                idct4_fix(r, 0.0);
                 for (int z = 0; z < 4; z++) at(z, y, x) = r[z];
             }
         }
@@ -518,7 +526,9 @@ bool build_plan(int cw, int ch, int cd, Plan& p) {
     double gd = 0.0;
     for (int n = 0; n < cs; n++) gd = std::max(gd, Kd[n] + J * L1d[n]);
     p.dec_G = G1 * (1.0 + 1e-3);
-    p.dec_E = 1e-12;
+    // + the last pass's offset form (idct8_fix / idct4_fix): at most three roundings of values in
+    // [2^20, 2^21), 2^-33 each, beyond what the analysis counts
+    p.dec_E = 1e-12 + 3.0 * std::ldexp(1.0, -33);
     // the kernel's byte packing reads floor(v) as a signed 16-bit value: |v| <= Bmax L1x must stay below
     // 2^15 - 1 (with room for the error terms)
     p.dec_l1_max = (float)(32000.0 / Bmax);

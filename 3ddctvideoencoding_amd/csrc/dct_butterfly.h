@@ -55,6 +55,11 @@ template <> DCT_HD double dfmac<double>(double c, const double& a, const double&
 }
 // multiplication by an exact power of two (0.5): exact in floating point
 template <class T> DCT_HD T dhalf(const T& a) { return T(0.5) * a; }
+// negation: exact
+template <class T> DCT_HD T dneg(const T& a) { return -a; }
+// c*a + K and a/2 + K, one rounding (the decode's fixed-point offset; Tracked: c*a and a/2)
+template <class T> DCT_HD T dfmac_k(double c, const T& a, double K) { return dfmac(c, a, T(K)); }
+template <class T> DCT_HD T dhalf_k(const T& a, double K) { return dfmac(0.5, a, T(K)); }
 
 // ---- 8-point forward DCT-II (orthonormal), in place ---------------------------------------
 // dcsub: subtracted from (e0 + e1) before scaling (the encoder folds its cube-mean centring in
@@ -98,13 +103,34 @@ DCT_HD void fdct4(T (&x)[4], const T& dcsub) {
 //   E0 = C4(X0+X4) + (A X2 + B X6), E3 = C4(X0+X4) - (A X2 + B X6)
 //   E1 = C4(X0-X4) + (B X2 - A X6), E2 = C4(X0-X4) - (B X2 - A X6)
 //   O_n = sum_r M[r][n] X_{2r+1};  x_n = E_n + O_n, x_{7-n} = E_n - O_n
+// idct8: the C4 scale fused into the even combine (E = fma(C4, X0 +- X4, +-r)): 34 ops.
+// idct8_fix: the decode's last pass: p = fma(C4, X0 + X4, K), q = fma(C4, X0 - X4, K) put the
+// fixed-point offset K into every output at no cost (36 ops).  For the Tracked analysis dfmac_k is the
+// plain product C4 * s (K = 0); the offset form's three roundings in [2^20, 2^21) (p, E, x: <= 2^-33
+// each, instead of the relative roundings the analysis counts) are added by the planner (dec_E).
 template <class T>
 DCT_HD void idct8(T (&X)[8]) {
-    T p = dmulc(kC4, dadd(X[0], X[4]));
-    T q = dmulc(kC4, dsub(X[0], X[4]));
-    T r0 = dfmac(kB8, X[6], dmulc(kA8, X[2]));
-    T r1 = dfmac(-kA8, X[6], dmulc(kB8, X[2]));
-    T E0 = dadd(p, r0), E3 = dsub(p, r0), E1 = dadd(q, r1), E2 = dsub(q, r1);
+    const T s = dadd(X[0], X[4]), d = dsub(X[0], X[4]);
+    const T r0 = dfmac(kB8, X[6], dmulc(kA8, X[2]));
+    const T r1 = dfmac(-kA8, X[6], dmulc(kB8, X[2]));
+    const T E0 = dfmac(kC4, s, r0), E3 = dfmac(kC4, s, dneg(r0));
+    const T E1 = dfmac(kC4, d, r1), E2 = dfmac(kC4, d, dneg(r1));
+    T O0 = dfmac(kC7, X[7], dfmac(kC5, X[5], dfmac(kC3, X[3], dmulc(kC1, X[1]))));
+    T O1 = dfmac(-kC5, X[7], dfmac(-kC1, X[5], dfmac(-kC7, X[3], dmulc(kC3, X[1]))));
+    T O2 = dfmac(kC3, X[7], dfmac(kC7, X[5], dfmac(-kC1, X[3], dmulc(kC5, X[1]))));
+    T O3 = dfmac(-kC1, X[7], dfmac(kC3, X[5], dfmac(-kC5, X[3], dmulc(kC7, X[1]))));
+    X[0] = dadd(E0, O0); X[7] = dsub(E0, O0);
+    X[1] = dadd(E1, O1); X[6] = dsub(E1, O1);
+    X[2] = dadd(E2, O2); X[5] = dsub(E2, O2);
+    X[3] = dadd(E3, O3); X[4] = dsub(E3, O3);
+}
+template <class T>
+DCT_HD void idct8_fix(T (&X)[8], double K) {
+    const T p = dfmac_k(kC4, dadd(X[0], X[4]), K);
+    const T q = dfmac_k(kC4, dsub(X[0], X[4]), K);
+    const T r0 = dfmac(kB8, X[6], dmulc(kA8, X[2]));
+    const T r1 = dfmac(-kA8, X[6], dmulc(kB8, X[2]));
+    const T E0 = dadd(p, r0), E3 = dsub(p, r0), E1 = dadd(q, r1), E2 = dsub(q, r1);
     T O0 = dfmac(kC7, X[7], dfmac(kC5, X[5], dfmac(kC3, X[3], dmulc(kC1, X[1]))));
     T O1 = dfmac(-kC5, X[7], dfmac(-kC1, X[5], dfmac(-kC7, X[3], dmulc(kC3, X[1]))));
     T O2 = dfmac(kC3, X[7], dfmac(kC7, X[5], dfmac(-kC1, X[3], dmulc(kC5, X[1]))));
@@ -125,6 +151,16 @@ DCT_HD void idct4(T (&X)[4]) {
     X[0] = dadd(E0, O0); X[3] = dsub(E0, O0);
     X[1] = dadd(E1, O1); X[2] = dsub(E1, O1);
 }
+// the decode's last pass at depth 4: E = fma(1/2, X0 +- X2, K) (Tracked: the exact halving; the offset
+// form's two roundings in [2^20, 2^21) are covered by the planner's dec_E as for idct8_fix)
+template <class T>
+DCT_HD void idct4_fix(T (&X)[4], double K) {
+    T E0 = dhalf_k(dadd(X[0], X[2]), K), E1 = dhalf_k(dsub(X[0], X[2]), K);
+    T O0 = dfmac(kQ4, X[3], dmulc(kP4, X[1]));
+    T O1 = dfmac(-kP4, X[3], dmulc(kQ4, X[1]));
+    X[0] = dadd(E0, O0); X[3] = dsub(E0, O0);
+    X[1] = dadd(E1, O1); X[2] = dsub(E1, O1);
+}
 
 // depth-generic forward / inverse along one axis
 template <int N, bool EXF, bool HAS_DCSUB, class T>
@@ -136,6 +172,11 @@ template <int N, class T>
 DCT_HD void idctN(T (&x)[N]) {
     if constexpr (N == 8) idct8(x);
     else idct4(x);
+}
+template <int N, class T>
+DCT_HD void idctN_fix(T (&x)[N], double K) {
+    if constexpr (N == 8) idct8_fix(x, K);
+    else idct4_fix(x, K);
 }
 
 }  // namespace dct3d
