@@ -4,14 +4,17 @@
 BASELINE.json metric: 8x8x8 cubes/s (encode DCT+quant) on 1080p x 8-frame stacks; % HBM roofline.
 Workload (config 2): 1920x1080 grayscale, 8-frame stacks, forward 3D DCT + quantise, B = 128
 device-resident stacks per step per GPU (4,147,200 cubes).  One step = one
-dct3d_encode_stacks_dev call over the batch (counter reset + fused encode kernel + exact-fold fixup
-kernel), inputs resident in HBM (synthetic, generated on device).  N GPUs: one process per GPU
-(torch.distributed.run), each encodes its own 128 stacks (weak scaling, no data-path collective);
-barrier + synchronize bracket the K timed steps, the time is the max over ranks.
+dct3d_encode_stacks_dev call over the batch (8x8x8: ONE launch of the fused encode kernel, which
+replays its rare uncertified coefficients itself), inputs resident in HBM (synthetic, generated on
+device).  N GPUs: one process per GPU (torch.distributed.run), each encodes its own 128 stacks (weak
+scaling, no data-path collective); config c4_encode_4k is one job of 64 4K stacks split over the
+ranks (strong scaling).  Barrier + synchronize bracket the K timed steps, the time is the max over
+ranks.
 
-Prints ONE JSON line (rank 0) with `roofline` (dominant kernel = the fused encode kernel, its
-average duration from HIP events recorded by the library around every launch in the timed region)
-and `cpu_baseline` (the Java-algorithm restatement, oracle/, timed on the host cores at N=1).
+Prints ONE JSON line (rank 0) with `roofline` (algorithmic bytes of a step / device time per step,
+from HIP events on the bench stream around the timed region; the dominant kernel's own rate as
+kernel_only_*), `ceiling` (this device's rates for the same traffic: memory-only twins, probes) and
+`cpu_baseline` (the Java-algorithm restatement, oracle/, timed on the host cores at N=1).
 """
 from __future__ import annotations
 
