@@ -1,35 +1,31 @@
-// dct3d_kernels.hip -- CDNA4 (gfx950) kernels of the 3D-DCT hot path.
+// dct3d_kernels.hip -- CDNA4 (gfx950) kernels of the 3D-DCT hot path (the device templates live in
+// dct3d_encode_dev.h / dct3d_decode_dev.h; this file instantiates them, adds the fused Exp-Golomb
+// kernels and the launchers).
 //
-// Work decomposition.  The 8x8x4 encode (and the 8-lane 8x8x8 form, variant 1): one wave64 owns 8
-// cubes, 8 lanes per cube.
-//   "row layout"  lane (c, y)        holds a[z][x]   (D x 8 values): the cube's row y of every frame
-//   "face layout" lane (c, kz[,h])   holds b[y][x]   (8 x 8 or 8 x 4 values): one z-face (or half)
-// The default 8x8x8 encode (encode16_kernel), the decode and the float drop-ins: 16 lanes per cube
-// (2 D lanes for 8x8x4 decode), 32 values per lane, the permlane16 pair (l, l ^ 16) splitting each cube
-// (DecGeom; encode16_kernel's comment has its three layouts).
-// Two of the three separable 8-point passes run in registers in one layout, the third in the other;
-// the single layout change is a wave-private LDS transpose (no workgroup barrier: one wave writes
-// and reads its own region, LDS ops of a wave execute in order).  Cube-major int32 / fp64 traffic is
-// staged through the same LDS region so every global access of the wave is a contiguous 1 KiB
-// (16 B per lane) burst; the u8 raster side is 8 B per lane, 8 rows x 64 B per instruction.
+// Work decomposition.  8x8x8 encode (encode16_kernel), decode, float drop-ins: 16 lanes per cube (2 D
+// lanes at 8x8x4 decode), 32 values per lane, the permlane16 pair (l, l ^ 16) splitting each cube.
+// 8x8x4 encode and the fused encode + Exp-Golomb: 8 lanes per cube, 8 cubes per wave ("row layout"
+// lane (c, y) holds a[z][x]; "face layout" lane (c, kz[, h]) holds b[y][x]).  Layout changes are
+// permlane16 swaps or a wave-private LDS transpose (no workgroup barrier: LDS ops of a wave execute in
+// order); cube-major int32 / fp64 traffic is staged through the same region so that every global
+// access of the wave is a contiguous 1 KiB (16 B per lane) burst.
 //
-// Encode (raster u8 -> quantised int32 cube-major), fp32, certified:
-//   load rows (row layout) -> cube sum S, mean m, A = max|x - m| (xor-shuffles over the 8 lanes)
-//   -> pass X (exact integer front, centring folded into X0) -> pass Z -> LDS transpose
-//   -> pass Y (face layout) -> quantise: q = v * fp32(1/step), n = rint(q), certify |q - n| < thr_s
-//   where thr_s = 0.5 - (A*G_s + E_s) (dct3d_plan.cpp) -> LDS staging -> 1 KiB coalesced stores.
-//   DC = JavaRound(fp64(S) * coef_dc) exactly (the Java fold of the single DC group).
-//   Uncertified coefficients are appended to a flag list; encode_fixup_kernel replays the Java fold.
-// Decode (quantised int32 cube-major -> raster u8), fp64, certified:
-//   staged 1 KiB loads -> face layout -> dequantise -> inverse pass Y -> LDS transpose (4 quarter
-//   rounds, 16 B per lane-slot) -> inverse pass X -> inverse pass Z -> certify (no integer within
-//   the bound of the pixel value in [1,255]) -> clamp, truncate (Decoder.java:112) -> 8 B row stores.
+// Encode (raster u8 -> quantised int32 cube-major), fp32, certified: rows -> S, m, A = max|x - m| ->
+// pass X (exact integer front, centring folded into X0) -> pass Z -> pass Y -> q = v * fp32(1/step),
+// n = rint(q), certified iff |q - n| < 0.5 - (A*G_s + E_s) (dct3d_plan.cpp).  DC = JavaRound(fp64(S) *
+// coef_dc) exactly.  Open coefficients: 8x8x8 settles them in the wave (fp64 second certificate, then
+// the exact Java fold); 8x8x4 appends them to a flag list for encode_fixup_kernel.
+// Decode (quantised int32 cube-major -> raster u8), fp64, certified: staged loads -> fp64 dequantise +
+// L1 -> inverse passes Y, X, Z (the last one adds the fixed-point offset) -> certificate on the low
+// words, 16-bit floors saturated to bytes -> raster stores; uncertified cubes are replayed whole in the
+// wave (exact Java InverseDCT fold) before the stores.
 #include "dct3d_encode_dev.h"
 #include "dct3d_decode_dev.h"
 
 namespace dct3d {
 
-// One wave per uncertified coefficient (flag list), then every coefficient of the whole-cube list.
+// 8x8x4 encode: one wave per uncertified coefficient (flag list), then every coefficient of the
+// whole-cube list (flag-list overflow).
 template <int D>
 __global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
     constexpr int CS = 64 * D;
