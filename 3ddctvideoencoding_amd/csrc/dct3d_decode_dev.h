@@ -150,12 +150,15 @@ __device__ __forceinline__ void dec_b_to_c(const double (&b)[8][4], double (&cz)
     }
 }
 
-// ---- exact replay of one uncertified cube (InverseDCT.java:56-66 / Decoder.java:107-117: for each pixel,
+// ---- exact replay of one lane's 32 pixels (InverseDCT.java:56-66 / Decoder.java:107-117: for each pixel,
 //      k ascending, zero coefficients skipped, acc = acc + c_k * coef[n][k] with both operations rounded,
 //      then clamp to [0, 255] and the (int) / (byte) truncation).  The whole wave: reload() puts the
-//      cube's dequantised coefficients in LDS (cf[k] = q_k * step_k, exact), lane l folds pixels
-//      l + 64 i reading the transposed table (coalesced, L2-resident), and the bytes land in LDS after
-//      cf.  Not inlined: the main path's register allocation stays its own. ----
+//      cube's dequantised coefficients in LDS (cf[k] = q_k * step_k, exact), the non-zero k go to an
+//      ascending list, then lane p < 32 folds pixel p of lane `src` (layout C: D=8 z = p/4, x = 4h + p%4;
+//      D=4 z = p/8, x = p%8), its table reads batched 8 at a time ahead of the sequential fold; the bytes
+//      land in LDS in lane src's word order.  A cube's certificate fails at one pixel in practice, so
+//      the replay is one lane's 32 pixels, not the cube's 512 (a dense cube's whole-cube fold took
+//      ~0.4 ms: a kernel tail).  Not inlined: the main path's register allocation stays its own. ----
 template <int D>
 struct ReloadCubes {  // from the int32 cube-major input
     const int32_t* in;
@@ -171,10 +174,10 @@ struct ReloadCubes {  // from the int32 cube-major input
 };
 
 template <int D, class Reload>
-__device__ __attribute__((noinline)) const uint8_t* decode_replay_cube(const double* inv_coef_t, Reload reload,
-                                                                       char* wl, int lane, uint32_t g) {
-    constexpr int CS = 64 * D, NP = CS / 64, U = 16 / NP;  // 16 table loads in flight per round
-    static_assert(CS * 8 + CS * 2 + CS <= kDecWaveLds, "replay scratch fits the wave's region");
+__device__ __attribute__((noinline)) const uint8_t* decode_replay_lane(const double* inv_coef_t, Reload reload,
+                                                                       char* wl, int lane, uint32_t g, int src) {
+    constexpr int CS = 64 * D, NP = CS / 64, B = 8;
+    static_assert(CS * 8 + CS * 2 + 32 <= kDecWaveLds, "replay scratch fits the wave's region");
     double* cf = (double*)wl;
     uint16_t* nzk = (uint16_t*)(wl + CS * 8);
     uint8_t* ob = (uint8_t*)(wl + CS * 10);
@@ -191,30 +194,29 @@ __device__ __attribute__((noinline)) const uint8_t* decode_replay_cube(const dou
         nnz += (uint32_t)__builtin_popcountll(bm);
     }
     wave_lds_sync();
-    double acc[NP];
+    if (lane < 32) {
+        const int sk = src & (D - 1), sh = (src >> 4) & 1;
+        const int y = (D == 8) ? sk : 4 * sh + sk;
+        const int z = (D == 8) ? lane >> 2 : lane >> 3;
+        const int x = (D == 8) ? 4 * sh + (lane & 3) : lane & 7;
+        const double* col = inv_coef_t + (z * 64 + y * 8 + x);  // coef[n][k] at col[k * CS]
+        double acc = 0.0;
+        for (uint32_t j = 0; j < nnz; j += B) {
+            double t[B];
+            uint32_t kk[B];
 #pragma unroll
-    for (int i = 0; i < NP; i++) acc[i] = 0.0;
-    const double* tab = inv_coef_t + lane;
-    // U coefficients per round with all their table loads in flight; a padded slot (past nnz) multiplies
-    // by 0 and adds +-0, which leaves acc's value unchanged
-    for (uint32_t j = 0; j < nnz; j += U) {
-        double cv[U], t[U][NP];
+            for (int u = 0; u < B; u++) {  // a padded slot (past nnz) re-reads the last k and adds +-0
+                kk[u] = nzk[min(j + u, nnz - 1)];
+                t[u] = col[(size_t)kk[u] * CS];
+            }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint32_t kk = nzk[min(j + u, nnz - 1)];
-            cv[u] = j + u < nnz ? cf[kk] : 0.0;
-#pragma unroll
-            for (int i = 0; i < NP; i++) t[u][i] = tab[(size_t)kk * CS + 64 * i];
+            for (int u = 0; u < B; u++) {
+                const double cv = j + u < nnz ? cf[kk[u]] : 0.0;
+                acc = __dadd_rn(acc, __dmul_rn(cv, t[u]));
+            }
         }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-#pragma unroll
-            for (int i = 0; i < NP; i++) acc[i] = __dadd_rn(acc[i], __dmul_rn(cv[u], t[u][i]));
-    }
-#pragma unroll
-    for (int i = 0; i < NP; i++) {
-        const double mn = acc[i] < 255.0 ? acc[i] : 255.0;
-        ob[lane + 64 * i] = (uint8_t)(int)(mn > 0.0 ? mn : 0.0);
+        const double mn = acc < 255.0 ? acc : 255.0;
+        ob[lane] = (uint8_t)(int)(mn > 0.0 ? mn : 0.0);
     }
     wave_lds_sync();
     return ob;
@@ -388,26 +390,24 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         }
     }
     flag |= (lo_min < mi) | (lo_max > 0xFFFFFFFFu - mi);
-    // ---- rare path: uncertified cubes (tens per 2e9 pixels) are replayed whole by the wave, before
-    //      the stores: the exact Java fold writes the cube's bytes to LDS and the owning lanes take
-    //      their words from there (no second store of any address, no flag list, no fixup launch) ----
+    // ---- rare path: a lane with an uncertified pixel (a few per 2e9 pixels) has its 32 pixels replayed
+    //      by the wave before the stores: the exact Java fold writes them to LDS and the lane takes its
+    //      words from there (no second store of any address, no flag list, no fixup launch) ----
     const unsigned long long fl = __ballot(flag && valid);
     if (__builtin_expect(fl != 0ull, 0)) {
         uint32_t nrep = 0;
-        for (int ci = 0; ci < CPW; ci++) {
-            const int base = (ci / (CPW / 2)) * 32 + (ci % (CPW / 2)) * D;
-            const unsigned long long cmask = ((unsigned long long)((1u << D) - 1) << base) |
-                                             ((unsigned long long)((1u << D) - 1) << (base + 16));
-            if ((fl & cmask) == 0ull) continue;  // wave-uniform
-            const uint8_t* ob = decode_replay_cube<D>(P.inv_coef_t, reload, wl, lane, cube0 + ci);
-            if (c == ci) {
+        for (unsigned long long rem = fl; rem != 0ull; rem &= rem - 1ull) {  // wave-uniform
+            const int src = (int)__builtin_ctzll(rem);
+            const int ci = (src >> 5) * (CPW / 2) + ((src & 15) / D);
+            const uint8_t* ob = decode_replay_lane<D>(P.inv_coef_t, reload, wl, lane, cube0 + ci, src);
+            if (lane == src) {
 #pragma unroll
                 for (int z = 0; z < D; z++)
 #pragma unroll
-                    for (int wd = 0; wd < NXC / 4; wd++) outw[z][wd] = *(const uint32_t*)(ob + z * 64 + y * 8 + x0 + 4 * wd);
+                    for (int wd = 0; wd < NXC / 4; wd++) outw[z][wd] = *(const uint32_t*)(ob + z * NXC + 4 * wd);
             }
             wave_lds_sync();
-            nrep++;
+            nrep += 32;
         }
         if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
     }

@@ -79,7 +79,6 @@ struct dct3d_ctx {
     DevBuf d_enc_counts;
     int enc_slot = 0;
     int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
-    bool last_count_decode = false;  // the slot holds a decode's whole-cube replays
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
@@ -359,10 +358,6 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
             st->n_flagged += w[i];
             st->n_rechecked += w[kCountSpread + i];
         }
-        if (c->last_count_decode) {  // decode: every replay is a whole cube
-            st->n_overflow_cubes = st->n_flagged;
-            st->n_flagged *= (uint64_t)c->plan.cs;
-        }
         return DCT3D_OK;
     } else if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
         return DCT3D_EDEVICE;
@@ -406,9 +401,8 @@ static void set_dec_replay(dct3d_ctx* c, DecodeParams& P) {
     P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
     P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
 }
-static void end_dec_replay(dct3d_ctx* c) {
+static void end_dec_replay(dct3d_ctx* c) {  // the slot counts replayed pixels (n_flagged)
     c->last_count_slot = c->enc_slot;
-    c->last_count_decode = true;
     c->enc_slot ^= 1;
 }
 
@@ -484,7 +478,6 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
             (void)hipEventRecord(ev[3], c->stream);
         }
         c->last_count_slot = c->enc_slot;
-        c->last_count_decode = false;
         c->enc_slot ^= 1;
         c->last_units = n_cubes * (uint64_t)c->plan.cs;
         c->last_valid = true;

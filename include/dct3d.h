@@ -67,9 +67,9 @@ typedef struct dct3d_ctx dct3d_ctx;
 /* Per-call statistics of the certify-or-replay scheme (last encode/decode call on the ctx). */
 typedef struct {
     uint64_t n_units;          /* coefficients (encode) or pixels (decode) produced by the last call */
-    uint64_t n_flagged;        /* units of the last call re-done by the exact Java fold */
-    uint64_t n_overflow_cubes; /* cubes of the last call re-done whole by the exact fold (decode: every
-                                  replay; 8x8x4 encode: the flag list was full) */
+    uint64_t n_flagged;        /* units of the last call re-done by the exact Java fold (decode: the 32
+                                  pixels of every lane with an uncertified pixel) */
+    uint64_t n_overflow_cubes; /* 8x8x4 encode: cubes of the last call re-done whole (flag list full) */
     /* HIP-event timing of every encode/decode call since dct3d_reset_timers (profiling on) */
     uint64_t n_timed;          /* calls timed */
     double kernel_ms_total;    /* main transform kernel, summed */
