@@ -227,6 +227,20 @@ constexpr int kTabN = 24;
 __device__ __forceinline__ void enc_tables(const EncodeParams& P, float4* tab, int lane) {
     if (lane < kTabN) tab[lane] = make_float4(P.tab_rstep[lane], P.tab_G[lane], 0.5f - P.tab_E[lane], 0.f);
 }
+// Descending rows (ky = 7 .. 0; e16_body): the first row reads its NB entries, each later row the one
+// entry that enters the window.
+template <int NB, int NI>
+__device__ __forceinline__ void tab_window_desc(const float4* tab, int& sz, int ky, float A, float (&rr)[NI],
+                                                float (&thr)[NI]) {
+    asm volatile("" : "+v"(sz));
+    const int hi = ky == 7 ? ky + NB - 1 : ky;
+#pragma unroll
+    for (int i = ky; i <= hi; i++) {
+        const float* t = (const float*)(tab + sz + i);
+        rr[i] = t[0];
+        thr[i] = __builtin_fmaf(-A, t[1], t[2]);
+    }
+}
 // Row ky of the quantise loop uses sums sz + ky .. sz + ky + NB - 1: the window slides by one entry per
 // row, read at the row's start (the opaque sz keeps the reads there), so 2 NB table registers are live
 // instead of 2 NI.
@@ -607,15 +621,19 @@ __device__ __forceinline__ void e16_body(const EncodeParams& P, const uint2 (&ra
     int sz = k + 4 * h;
     float rr[11], thr[11];
     fm = 0u;
+    // rows and columns in descending order, fm = 2 fm + open: one v_addc per coefficient (the compare's
+    // lane mask is the carry-in), and coefficient (ky, e) ends at bit 4 ky + e
 #pragma unroll
-    for (int ky = 0; ky < 8; ky++) {
+    for (int ky = 7; ky >= 0; ky--) {
         pin(b[ky]);
-        tab_window<4, 11>(tab, sz, ky, A, rr, thr);
+        tab_window_desc<4, 11>(tab, sz, ky, A, rr, thr);
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
+        for (int e = 3; e >= 0; e--) {
             const float qq = b[ky][e] * rr[ky + e];
             const float n = __builtin_rintf(qq);
-            fm |= (__builtin_fabsf(qq - n) >= thr[ky + e] ? 1u : 0u) << (4 * ky + e);
+            const unsigned long long open = __ballot(__builtin_fabsf(qq - n) >= thr[ky + e]);
+            unsigned long long cout;
+            asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(fm), "=s"(cout) : "v"(fm), "s"(open));
             qv[ky][e] = (int32_t)n;
         }
         pin(qv[ky]);
