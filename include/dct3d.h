@@ -73,7 +73,7 @@ typedef struct {
     /* HIP-event timing of every encode/decode call since dct3d_reset_timers (profiling on) */
     uint64_t n_timed;          /* calls timed */
     double kernel_ms_total;    /* main transform kernel, summed */
-    double fixup_ms_total;     /* exact-fold kernel, summed */
+    double fixup_ms_total;     /* exact-fold kernel (8x8x4 encode), summed; 0 for single-launch calls */
     uint64_t n_rechecked;      /* 8x8x8 encode: units of the last call the fp32 certificate left open
                                   and the fp64 second certificate settled (not counted in n_flagged) */
 } dct3d_stats;
@@ -122,9 +122,10 @@ int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_s
 /* Test / diagnostic options of a ctx.  Each one changes only HOW later calls reach their results
  * (the results stay bit-identical): tests use them to drive the rare paths.  value 0 restores the
  * default.  Unknown options: DCT3D_EINVAL. */
-#define DCT3D_OPT_FLAG_CAP 1          /* flag-list capacity in entries (8x8x4 encode, decode): overflow
-                                         sends cubes to the whole-cube replay */
-#define DCT3D_OPT_DEC_MARGIN 2        /* added to the decode certification margin: cubes go to the replay */
+#define DCT3D_OPT_FLAG_CAP 1          /* flag-list capacity in entries (8x8x4 encode): overflow sends cubes
+                                         to the whole-cube replay */
+#define DCT3D_OPT_DEC_MARGIN 2        /* added to the decode certification margin: lanes go to the in-wave
+                                         exact replay */
 #define DCT3D_OPT_ENC_NO_RECHECK 3    /* 1: the 8x8x8 encode skips its fp64 second certificate, so every
                                          coefficient the fp32 certificate leaves open takes the Java fold */
 #define DCT3D_OPT_EG_TWO_STEP 5       /* 1: dct3d_encode_eg / dct3d_decode_eg through int32 cubes */
