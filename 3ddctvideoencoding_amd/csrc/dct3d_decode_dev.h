@@ -222,6 +222,81 @@ __device__ __attribute__((noinline)) const uint8_t* decode_replay_lane(const dou
     return ob;
 }
 
+// the cube of a lane within its wave (decode layouts: lane = c2*32 + h*16 + c1*D + k)
+template <int D>
+__device__ __forceinline__ int dec_cube_of_lane(int lane) { return (lane >> 5) * (DecGeom<D>::CPW / 2) + ((lane & 15) / D); }
+
+// ---- stores of one tile's bytes (decode_tile; the memory-only twin in dct3d_diag.hip) ----
+// outw[z][wd]: lane (c, y, h)'s bytes of plane z (layout C: D=8 x 4h..4h+3 of row k; D=4 x 0..7 of
+// row 4h + k).  A full block (its 4 waves' 4 CPW consecutive cubes all exist; nbx even, so a 16-byte
+// pair of cubes never straddles a block-row) leaves through LDS: each wave puts its rows in its own
+// region ([z][y][CPW x 8 B]; every earlier use of the region is over), one barrier, then every 16-byte
+// chunk of the block's rows -- two cubes of one row of one plane -- goes out with a non-temporal store,
+// a wave instruction covering 1 KiB of whole 128-byte lines.  Per-lane 4- or 8-byte row pieces cost
+// ~1.5x the write time (profiles/r02/variant_sweep.txt).  Other blocks store per lane.  Every wave of
+// the block must call this (the barrier); a full block has no early-returning wave.
+template <int D>
+__device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
+                                               const uint32_t (&outw)[D][(D == 8) ? 1 : 2], bool valid) {
+    using G = DecGeom<D>;
+    constexpr int CPW = G::CPW;
+    constexpr int NXC = (D == 8) ? 4 : 8;
+    constexpr int W = CPW * 8;  // bytes of one row of the wave's cubes
+    const int h = (lane >> 4) & 1, k = lane & (D - 1);
+    const int y = (D == 8) ? k : (4 * h + k);
+    const int x0 = (D == 8) ? 4 * h : 0;
+    const int c = dec_cube_of_lane<D>(lane);
+    const int wave = (int)(threadIdx.x >> 6);
+    const uint32_t blk0 = cube0 - (uint32_t)wave * CPW;
+    if (P.blk_store && blk0 + kWavesPerBlock * CPW <= P.n_cubes) {  // block-uniform
+#pragma unroll
+        for (int z = 0; z < D; z++) {
+            char* t = wl + z * 8 * W + y * W + c * 8 + x0;
+            if constexpr (NXC == 4) *(uint32_t*)t = outw[z][0];
+            else *(uint2*)t = make_uint2(outw[z][0], outw[z][1]);
+        }
+        __syncthreads();
+        const char* lds0 = wl - wave * kDecWaveLds;
+        constexpr int CPR = kWavesPerBlock * W / 16;  // 16-byte chunks per block row
+        // the block's first cube, wave-uniform (scalar arithmetic); a block inside one block-row (every
+        // block when nbx is a multiple of 4 CPW) addresses its chunks from it directly
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk0);
+        const uint32_t s0 = fdiv(b0, P.div_cps);
+        const uint32_t rr0 = b0 - s0 * P.cubes_per_stack;
+        const uint32_t by0 = fdiv(rr0, P.div_nbx), bx0 = rr0 - by0 * P.nbx;
+        const bool one_row = bx0 + kWavesPerBlock * CPW <= P.nbx;
+        uint8_t* const base0 = P.out + (size_t)s0 * P.stack_stride + (size_t)(by0 * 8) * P.width + bx0 * 8;
+#pragma unroll
+        for (int i = 0; i < D * 8 * CPR / kBlock; i++) {
+            const int q = (int)threadIdx.x + kBlock * i;
+            const int z = q / (8 * CPR), r = q % (8 * CPR), yy = r / CPR, j = r % CPR;
+            const int4 v = *(const int4*)(lds0 + (j * 16 / W) * kDecWaveLds + z * 8 * W + yy * W + (j * 16) % W);
+            uint8_t* dst;
+            if (one_row) {
+                dst = base0 + ((uint32_t)z * (uint32_t)P.plane + (uint32_t)yy * P.width + (uint32_t)j * 16u);  // < 2^32 within a stack
+            } else {
+                const uint32_t gc = blk0 + 2 * j;
+                const uint32_t s = fdiv(gc, P.div_cps);
+                const uint32_t rr = gc - s * P.cubes_per_stack;
+                const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
+                dst = P.out + (size_t)s * P.stack_stride + (size_t)z * P.plane + (size_t)(by * 8 + yy) * P.width + bx * 8;
+            }
+            __builtin_nontemporal_store(i32x4_t{v.x, v.y, v.z, v.w}, (i32x4_t*)dst);
+        }
+    } else if (valid) {
+        const uint32_t g = cube0 + c;
+        const uint32_t s = fdiv(g, P.div_cps);
+        const uint32_t rr = g - s * P.cubes_per_stack;
+        const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
+        uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + y) * P.width + bx * 8 + x0;
+#pragma unroll
+        for (int z = 0; z < D; z++, dst += P.plane) {  // one 64-bit add per plane
+            if constexpr (NXC == 4) *(uint32_t*)dst = outw[z][0];
+            else *(uint2*)dst = make_uint2(outw[z][0], outw[z][1]);
+        }
+    }
+}
+
 // One tile (CPW cubes) from the staged input in the wave's LDS region to the raster.  after_a() runs
 // once the staged input is in registers (the persistent variant issues the next tile's loads there);
 // reload(g, cf, lane) re-reads cube g's dequantised coefficients for the rare exact replay.
@@ -411,17 +486,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         }
         if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
     }
-    if (valid) {
-        const uint32_t s = fdiv(g, P.div_cps);
-        const uint32_t rr = g - s * P.cubes_per_stack;
-        const uint32_t by = fdiv(rr, P.div_nbx), bx = rr - by * P.nbx;
-        uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + y) * P.width + bx * 8 + x0;
-#pragma unroll
-        for (int z = 0; z < D; z++, dst += P.plane) {  // one 64-bit add per plane
-            if constexpr (NXC == 4) *(uint32_t*)dst = outw[z][0];
-            else *(uint2*)dst = make_uint2(outw[z][0], outw[z][1]);
-        }
-    }
+    dec_store_tile<D>(P, wl, lane, cube0, outw, valid);
 }
 
 // Block 0 zeroes the next call's counter slot, both halves (the two slots alternate between the

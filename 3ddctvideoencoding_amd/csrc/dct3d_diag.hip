@@ -62,21 +62,21 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel_diag(DecodeParams P) 
     }
     dec_stage_tile<D>(wl, lane, v);
     wave_lds_sync();
-    if (MODE == 1) {
+    if (MODE == 1) {  // the product's loads, staging reads and stores (dec_store_tile), no transform
         const int h = (lane >> 4) & 1, k = lane & (D - 1);
         const int c = (lane >> 5) * (G::CPW / 2) + ((lane & 15) / D);
-        const uint32_t g = cube0 + c;
         uint32_t acc = 0;
         for (int ky = 0; ky < 8; ky++) {
             const int4 x = *(const int4*)(wl + c * G::SA_C + k * G::SA_F + h * 16 + ky * 32);
             acc += x.x ^ x.y ^ x.z ^ x.w;
         }
-        if (g < P.n_cubes) {
-            const uint32_t s = g / P.cubes_per_stack, rr = g - s * P.cubes_per_stack;
-            const uint32_t by = rr / P.nbx, bx = rr - by * P.nbx;
-            uint8_t* dst = P.out + (size_t)s * P.stack_stride + (size_t)(by * 8 + k) * P.width + bx * 8 + 4 * h;
-            for (int z = 0; z < D; z++) *(uint32_t*)(dst + (size_t)z * P.plane) = acc + z;
-        }
+        uint32_t outw[D][(D == 8) ? 1 : 2];
+#pragma unroll
+        for (int z = 0; z < D; z++)
+#pragma unroll
+            for (int wd = 0; wd < ((D == 8) ? 1 : 2); wd++) outw[z][wd] = acc + z + wd;
+        wave_lds_sync();
+        dec_store_tile<D>(P, wl, lane, cube0, outw, cube0 + c < P.n_cubes);
         return;
     }
     DecodeParams Q = P;
@@ -328,6 +328,7 @@ int dct3d_decode_diag_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
     P.stack_stride = P.plane * 8;
+    P.blk_store = mode == 1 && P.nbx % 2 == 0 && P.stack_stride < (1ull << 32) ? 1u : 0u;  // as the product (mode 2 stores nothing)
     P.inv_coef_t = nullptr;  // no replay: mode 1 certifies nothing, mode 2 stores (and so flags) nothing
     const uint32_t per = DecGeom<8>::CPW * kWavesPerBlock;
     const uint32_t groups = (uint32_t)((n_cubes + per - 1) / per);

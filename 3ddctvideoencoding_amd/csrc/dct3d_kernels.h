@@ -74,6 +74,7 @@ struct DecodeParams {
     uint64_t plane, stack_stride;
     double dec_G, dec_E;       // certificate: margin = dec_G * sum |dequantised| + dec_E
     float dec_l1_max;          // sum |dequantised| >= this: the cube goes to the exact replay
+    uint32_t blk_store;        // 1: full blocks store whole lines through LDS (nbx even, a stack < 4 GiB)
     // uncertified cubes are replayed whole inside the wave (exact Java InverseDCT fold)
     const double* inv_coef_t;    // [cs * cs], transposed: inv_coef_t[k * cs + n] = coefficients[n][k]
     unsigned int* replay_count;  // this call's counter slot: [0, S) cubes replayed (S = kCountSpread), or nullptr

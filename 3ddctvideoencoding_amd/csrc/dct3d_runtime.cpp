@@ -533,6 +533,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
     P.dec_l1_max = c->plan.dec_l1_max;
+    P.blk_store = (w / 8) % 2 == 0 && plane * D < (1ull << 32) ? 1u : 0u;  // dec_store_tile's conditions
     // test option: widen the certification margin so that most pixels are uncertified and their cubes
     // take the whole-cube replay path (tests/test_gpu_parity.py); a wider margin is never unsafe
     P.dec_E += c->opt_dec_margin;
@@ -1061,6 +1062,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     P.dec_G = c->plan.dec_G;
     P.dec_E = c->plan.dec_E;
     P.dec_l1_max = c->plan.dec_l1_max;
+    P.blk_store = (w / 8) % 2 == 0 && plane * D < (1ull << 32) ? 1u : 0u;  // dec_store_tile's conditions
     P.dec_E += c->opt_dec_margin;  // test option (see above)
     set_dec_replay(c, P);
     hipEvent_t* ev = timing_slot(c);
