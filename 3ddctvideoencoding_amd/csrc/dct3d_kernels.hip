@@ -354,7 +354,10 @@ __global__ __launch_bounds__(kBlock, 4) void cube_f32_kernel(const float* __rest
                 v[e] = (float)t;
             }
 #pragma unroll
-            for (int e = 0; e < NXC; e += 4) *(float4*)(o + z * 64 + e) = make_float4(v[e], v[e + 1], v[e + 2], v[e + 3]);
+            for (int e = 0; e < NXC; e += 4) {  // non-temporal: whole 128-byte lines, written once
+                typedef float f32x4_t __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(f32x4_t{v[e], v[e + 1], v[e + 2], v[e + 3]}, (f32x4_t*)(o + z * 64 + e));
+            }
         }
     }
 }
