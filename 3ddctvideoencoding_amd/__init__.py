@@ -29,7 +29,7 @@ INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 
 DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
 # test / diagnostic options (include/dct3d.h, Context.set_option)
-DCT3D_OPT_FLAG_CAP, DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 1, 2, 3, 5, 6
+DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 2, 3, 5, 6
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -61,8 +61,8 @@ class PlanInfo(C.Structure):
 
 
 class Stats(C.Structure):
-    _fields_ = [("n_units", C.c_uint64), ("n_flagged", C.c_uint64), ("n_overflow_cubes", C.c_uint64),
-                ("n_timed", C.c_uint64), ("kernel_ms_total", C.c_double), ("fixup_ms_total", C.c_double),
+    _fields_ = [("n_units", C.c_uint64), ("n_flagged", C.c_uint64),
+                ("n_timed", C.c_uint64), ("kernel_ms_total", C.c_double), ("aux_ms_total", C.c_double),
                 ("n_rechecked", C.c_uint64)]
 
     def as_dict(self) -> dict:

@@ -437,8 +437,6 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     // in one op.  A cube with a larger L1 (never from an encoder of 8-bit frames) goes to the replay.
     const double m = __builtin_fmin((double)l1_f * P.dec_G + P.dec_E, 0.5);
     const uint32_t mi = (uint32_t)__builtin_ceil(__fma_rn(m, 0x1p32, 0.5)) + 1u;  // + 1: m's own rounding
-    const int y = (D == 8) ? k : (4 * h + k);
-    const int x0 = (D == 8) ? 4 * h : 0;
     bool flag = !(l1_f < P.dec_l1_max);
     uint32_t lo_min = 0xFFFFFFFFu, lo_max = 0u;
     uint32_t outw[D][NXC / 4];

@@ -21,7 +21,7 @@ struct LdsBits {
         return i < n ? v : 0u;
     }
 };
-// the stream in global memory (the decode fixup's re-parse of a replayed cube: rare, latency-bound)
+// the stream in global memory (the fused decode's re-parse of a replayed cube: rare, latency-bound)
 struct GlobalBits {
     const uint32_t* w;
     uint64_t nw;

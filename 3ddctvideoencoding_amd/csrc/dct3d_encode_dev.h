@@ -257,12 +257,87 @@ __device__ __forceinline__ void tab_window(const float4* tab, int& sz, int ky, f
     }
 }
 
-// Everything after the row loads, for the 8 cubes from cube0: statistics, transform, quantise +
-// certify, staged 1 KiB stores, uncertified coefficients to the flag list.
+// 8x8x4 exact Java fold of the coefficients the certificate left open (exact ties: the 4-point k = 2
+// basis row is +-1/2, so (kz = 2, ky, kx in {0, 4}) values can be rational x.5 exactly -- about one
+// coefficient in 10^4 on ramp content), the wave's 8 cubes in parallel.  Per round, the 8 lanes of
+// cube c take one of its open coefficients k (DCT.java:44-52): lane j sums its row (y = j of frames
+// 0..3, px) into the cube's group sums by LDS integer atomics (exact), forms the products of groups
+// j, j + 8, ... (one correctly rounded fp64 multiply each, as in Java), and lane 0 of the cube folds
+// them in HashMap order, divides by the step and rounds (Math.round), writing the result over the
+// stored value.  Rounds = the most open coefficients of any one cube (the whole-wave exact_coef of
+// encode16_kernel runs one coefficient per round).  Scratch: the wave's staging region, free again
+// after the stores: kGM4 int sums + kGM4 fp64 products per cube.
+constexpr int kGM4 = kGM4Dev;  // >= the most Java groups of any 8x8x4 coefficient (40; the plan checks it)
+static_assert(8 * kGM4 * (4 + 8) <= enc_wave_lds<4>(), "8x8x4 replay scratch fits the wave's region");
+__device__ __forceinline__ void enc4_replay(const EncodeParams& P, const uint2 (&px)[4], uint32_t fm, char* wl,
+                                            int lane, uint32_t cube0) {
+    constexpr int CS = 256;
+    const int c = lane >> 3, j = lane & 7;
+    int* const ssum = (int*)wl + c * kGM4;
+    double* const prod = (double*)(wl + 8 * kGM4 * 4) + c * kGM4;
+    uint32_t nrep = 0;
+    for (;;) {
+        const uint64_t who = __ballot(fm != 0u);
+        if (who == 0ull) break;
+        const uint32_t mine = (uint32_t)(who >> (8 * c)) & 0xFFu;  // lanes of this cube still open
+        const bool act = mine != 0u;
+        const int src = 8 * c + (act ? __builtin_ctz(mine) : 0);
+        const int bit = __shfl(fm ? __builtin_ctz(fm) : 0, src, 64);
+        const int sj = src & 7;
+        const int kz = sj >> 1, ky = bit >> 2, kx = (sj & 1) * 4 + (bit & 3);
+        const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx);
+        // (lean: loops rolled and the coefficients loaded where used -- an unrolled body cost 20 VGPRs
+        // over the whole kernel, i.e. occupancy)
+        int ng = 0;
+        uint2 gr[4];
+        if (act) {
+            ng = P.ngroups[k];
+#pragma unroll
+            for (int z = 0; z < 4; z++) gr[z] = *(const uint2*)(P.group_of + (size_t)k * CS + (z * 8 + j) * 8);
+#pragma unroll 1
+            for (int i = j; i < kGM4; i += 8) ssum[i] = 0;
+        }
+        wave_lds_sync();
+        if (act) {
+#pragma unroll
+            for (int z = 0; z < 4; z++) {
+                const uint2 gz = gr[z], pz = px[z];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int g0 = (int)((gz.x >> (8 * e)) & 0xFFu), g1 = (int)((gz.y >> (8 * e)) & 0xFFu);
+                    if (g0 < ng) atomicAdd(&ssum[g0], (int)((pz.x >> (8 * e)) & 0xFFu));
+                    if (g1 < ng) atomicAdd(&ssum[g1], (int)((pz.y >> (8 * e)) & 0xFFu));
+                }
+            }
+        }
+        wave_lds_sync();
+        if (act) {
+#pragma unroll 1
+            for (int i = j; i < ng; i += 8)
+                prod[i] = __dmul_rn((double)ssum[i], P.coef[(size_t)k * kMaxGroupsDev + i]);
+        }
+        wave_lds_sync();
+        if (act && j == 0) {
+            double acc = 0.0;
+#pragma unroll 1
+            for (int gi = 0; gi < ng; gi++) acc = __dadd_rn(acc, prod[gi]);  // DCT.java:50, in order
+            const int q = java_round_dev(__ddiv_rn(acc, (double)max(1, 5 * (kx + ky + kz))));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after this lane's staged store of the word
+            P.out[(size_t)(cube0 + c) * CS + k] = q;
+        }
+        nrep += (uint32_t)__builtin_popcountll(__ballot(act && j == 0));
+        if (act && lane == src) fm &= fm - 1u;
+        wave_lds_sync();  // the next round rewrites the sums
+    }
+    if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
+}
+
+// Everything after the row loads, for the 8 cubes from cube0 (8x8x4): statistics, transform, quantise +
+// certify, staged 1 KiB stores, the exact fold of the uncertified coefficients (enc4_replay).
 template <int D, bool NT>
 __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (&raw)[D], char* wl,
                                             const float4* tab, int lane, uint32_t cube0) {
-    constexpr int CS = 64 * D;
+    static_assert(D == 4, "8x8x8 encodes in encode16_kernel");
     constexpr int NB = (D == 8) ? 8 : 4;      // kx values per lane in the face layout
     constexpr int NI = 7 + NB;                // distinct (ky + kx') sums per lane
     const int c = lane >> 3, j = lane & 7;
@@ -285,15 +360,11 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
 
     // ---- quantise + certify (thr_s = 0.5 - (A*G_s + E_s), dct3d_plan.cpp) ----
     // The per-lane tables are read row by row from the block's LDS copy (enc_tables, tab_window).
+    // Uncertified coefficients: the lane's mask fm, bit ky * 4 + x (coefficient (kz, ky, kx0 + x)).
     int sz = so;
     float rr[NI], thr[NI];
-    // Uncertified coefficients: 8x8x4 (INL) appends them to the flag list inside the row loop while
-    // q is in registers -- its exact ties (the 4-point k = 2 row is +-1/2) flag a quarter of the
-    // waves; 8x8x8 (flags in ~5 % of waves, registers at the 128 limit) re-derives them after the
-    // stores from reloaded rows instead.
-    constexpr bool INL = (D == 4);
     int32_t qv[8][NB];
-    int overflow = 0, flag = 0;
+    uint32_t fm = 0u;
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         pin(b[ky]);
@@ -307,60 +378,30 @@ __device__ __forceinline__ void encode_body(const EncodeParams& P, const uint2 (
             f |= __builtin_fabsf(qq[x] - n) >= thr[ky + x];
             qv[ky][x] = (int32_t)n;
         }
-        if (!INL) flag |= (int)f;
-        if (INL && __builtin_expect(f && valid, 0)) {
+        if (__builtin_expect(f, 0)) {
+            uint32_t bits = 0;
 #pragma unroll
             for (int x = 0; x < NB; x++)
-                if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) {
-                    const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
-                    const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                    if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
-                    else overflow = 1;
-                }
+                if (__builtin_fabsf(qq[x] - __builtin_rintf(qq[x])) >= thr[ky + x]) bits |= 1u << x;
+            fm |= bits << (ky * NB);
         }
         pin(qv[ky]);
-        asm volatile("" : "+v"(overflow), "+v"(flag));  // the row's checks complete here (q, n die)
+        asm volatile("" : "+v"(fm));  // the row's checks complete here (q, n die)
     }
-    if (j == 0) qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+    if (j == 0) {
+        qv[0][0] = java_round_dev((double)S * P.coef_dc);  // exact DC (single Java group)
+        fm &= ~1u;
+    }
+    if (!valid) fm = 0u;
 
     enc_stage_store<D, NT>(P, qv, wl, lane, cube0);
 
-    // ---- !INL rare path: identify uncertified coefficients (recomputed from reloaded rows) ----
-    if (!INL && __builtin_expect(__ballot(flag && valid) != 0ull, 0)) {
-        uint2 raw2[D];
-        load_rows<D>(P, g, valid, j, raw2);
-        float a2[D][8];
-        to_float<D>(raw2, a2);
-        float b2[8][NB];
-        forward_cube<D, NB>(a2, m, c, j, wl, b2);
-        if (flag && valid) {
-#pragma unroll
-            for (int ky = 0; ky < 8; ky++)
-#pragma unroll
-                for (int x = 0; x < NB; x++) {
-                    const float th2 = __builtin_fmaf(-A, P.tab_G[so + ky + x], 0.5f - P.tab_E[so + ky + x]);
-                    const float q = b2[ky][x] * rr[ky + x];
-                    const float n = __builtin_rintf(q);
-                    if (__builtin_fabsf(q - n) >= th2) {
-                        const uint32_t k = (uint32_t)((kz * 8 + ky) * 8 + kx0 + x);
-                        const uint32_t idx = atomicAdd(&P.counters[0], 1u);
-                        if (idx < P.flag_cap) P.flag_list[idx] = (unsigned long long)g * CS + k;
-                        else overflow = 1;
-                    }
-                }
-        }
-        wave_lds_sync();
+    // rare path: the rows again (after the stores: held across them they cost occupancy), the fold
+    if (__builtin_expect(__ballot(fm != 0u) != 0ull, 0)) {  // wave-uniform
+        uint2 px[D];
+        load_rows<D>(P, g, valid, j, px);
+        enc4_replay(P, px, fm, wl, lane, cube0);
     }
-    // ---- flag-list overflow: the cube goes to the whole-cube replay (one entry per cube) ----
-    const unsigned long long ov = __ballot(overflow != 0);
-    if (__builtin_expect(ov != 0ull, 0)) {
-        const uint32_t mine = (uint32_t)(ov >> (c * 8)) & 0xFFu;
-        if (overflow && (__builtin_ctz(mine) == j)) {
-            const uint32_t idx = atomicAdd(&P.counters[1], 1u);
-            P.cube_list[idx] = g;  // capacity n_cubes: never overflows
-        }
-    }
-
 }
 
 // One wave = one group of 8 consecutive cubes (register-prefetch loops over several groups spill
@@ -373,6 +414,10 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
     uint2 raw[D];
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
+    if (blockIdx.x == 0 && P.replay_clear) {
+#pragma unroll
+        for (int i = 0; i < 2 * kCountSpread / kBlock; i++) P.replay_clear[i * kBlock + threadIdx.x] = 0u;
+    }
     if (cube0 >= P.n_cubes) return;  // wave-uniform
     enc_tables(P, s_tab, lane);
     encode_body<D, NT>(P, raw, lds + wave * enc_wave_lds<D>(), s_tab, lane, cube0);

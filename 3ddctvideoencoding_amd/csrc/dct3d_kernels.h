@@ -8,6 +8,7 @@
 namespace dct3d {
 
 constexpr int kMaxGroupsDev = 64;  // == kMaxGroups in dct3d_plan.h; one LDS slot per lane
+constexpr int kGM4Dev = 48;        // == kMaxGroups4 in dct3d_plan.h (8x8x4 in-wave fold, per cube)
 // Per-call counters of the in-wave paths are spread over kCountSpread words per counter (a block adds
 // to word blockIdx & (kCountSpread - 1)): 10^5 same-address atomics per call serialise at the L2
 // (~12 ns each, longer than the whole kernel); the host sums the words.
@@ -35,34 +36,15 @@ struct EncodeParams {
     const float* tab_rstep;    // [32] fp32(1/step_s)
     const float* tab_G;        // [32]
     const float* tab_E;        // [32]
-    // 8x8x4 (encode_kernel): uncertified coefficients go to a flag list for encode_fixup_kernel
-    unsigned long long* flag_list;
-    unsigned int* counters;    // [0] flagged coefficients, [1] overflow cubes
-    uint32_t flag_cap;
-    uint32_t* cube_list;       // capacity n_cubes
-    // 8x8x8 (encode16_kernel): uncertified coefficients replayed inside the wave (exact Java fold)
-    const int32_t* ngroups;    // [cs] exact replay tables (as FixupParams)
+    // uncertified coefficients are replayed inside the wave (exact Java fold, DCT.java:44-52)
+    const int32_t* ngroups;    // [cs] fold length of each coefficient
     const double* coef;        // [cs * kMaxGroupsDev]
     const uint8_t* group_of;   // [cs * cs]
     unsigned int* replay_count;  // this call's counter slot: [0, S) Java-fold replays, [S, 2S) fp64
                                  // settlements (S = kCountSpread words each), or nullptr
     unsigned int* replay_clear;  // the other slot (2S words): zeroed by block 0 for the next call
-    const double* tab64;       // second certificate: [64] fp64 basis [k][n], [32] thresholds per s
+    const double* tab64;       // 8x8x8 second certificate: [64] fp64 basis [k][n], [32] thresholds per s
     uint32_t recheck;          // 1: run the second certificate (0: test option, all open -> Java fold)
-};
-
-struct FixupParams {
-    const uint8_t* raster;
-    int32_t* out;
-    uint32_t cubes_per_stack, nbx, width;
-    uint64_t plane, stack_stride;
-    const unsigned long long* flag_list;
-    const unsigned int* counters;
-    uint32_t flag_cap;
-    const uint32_t* cube_list;
-    const int32_t* ngroups;    // [cs]
-    const double* coef;        // [cs * kMaxGroupsDev]
-    const uint8_t* group_of;   // [cs * cs]
 };
 
 struct DecodeParams {
@@ -91,10 +73,6 @@ struct Fwd64Params {
 int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st);
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
 int launch_encode(int D, const EncodeParams& P, hipStream_t st);
-// true when launch_encode(D) replays uncertified coefficients itself (encode16_kernel: 8x8x8), i.e. the
-// call needs no counter reset and no encode_fixup_kernel
-bool encode_replays_inwave(int D);
-int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st);
 struct EgParams {
     const int32_t* q;          // cube-major quantised values
     uint64_t n_cubes;
@@ -134,7 +112,7 @@ struct EgDecParams {
 // cubes coded straight into a private slot (no int32 cube-major round trip).  Segment = one wave = 8
 // consecutive cubes; lane l codes 1/8 of one cube's diagonal stream into its words of the slot.
 struct EgFusedParams {
-    const int32_t* ngroups;    // exact replay tables (as FixupParams)
+    const int32_t* ngroups;    // exact replay tables (as EncodeParams)
     const double* coef;
     const uint8_t* group_of;
     const uint16_t* diag;      // [cs] stream position -> cube index

@@ -14,7 +14,7 @@
 // pass X (exact integer front, centring folded into X0) -> pass Z -> pass Y -> q = v * fp32(1/step),
 // n = rint(q), certified iff |q - n| < 0.5 - (A*G_s + E_s) (dct3d_plan.cpp).  DC = JavaRound(fp64(S) *
 // coef_dc) exactly.  Open coefficients: 8x8x8 settles them in the wave (fp64 second certificate, then
-// the exact Java fold); 8x8x4 appends them to a flag list for encode_fixup_kernel.
+// the exact Java fold); 8x8x4 folds them exactly in the wave, its 8 cubes in parallel (enc4_replay).
 // Decode (quantised int32 cube-major -> raster u8), fp64, certified: staged loads -> fp64 dequantise +
 // L1 -> inverse passes Y, X, Z (the last one adds the fixed-point offset) -> certificate on the low
 // words, 16-bit floors saturated to bytes -> raster stores; uncertified cubes are replayed whole in the
@@ -23,36 +23,6 @@
 #include "dct3d_decode_dev.h"
 
 namespace dct3d {
-
-// 8x8x4 encode: one wave per uncertified coefficient (flag list), then every coefficient of the
-// whole-cube list (flag-list overflow).
-template <int D>
-__global__ __launch_bounds__(256) void encode_fixup_kernel(FixupParams P) {
-    constexpr int CS = 64 * D;
-    __shared__ int Ssum[4][kMaxGroupsDev];
-    __shared__ double prod[4][kMaxGroupsDev];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
-                       P.ngroups, P.coef, P.group_of};
-    const uint32_t nf = min(P.counters[0], P.flag_cap);
-    const uint32_t ncube = P.counters[1];
-    const unsigned long long total = (unsigned long long)nf + (unsigned long long)ncube * CS;
-    for (unsigned long long e = (unsigned long long)blockIdx.x * 4 + wave; e < total;
-         e += (unsigned long long)gridDim.x * 4) {
-        uint32_t g, k;
-        if (e < nf) {
-            const unsigned long long v = P.flag_list[e];
-            g = (uint32_t)(v / CS);
-            k = (uint32_t)(v % CS);
-        } else {
-            const unsigned long long e2 = e - nf;
-            g = P.cube_list[e2 / CS];
-            k = (uint32_t)(e2 % CS);
-        }
-        const int q = exact_coef<D>(R, g, k, lane, Ssum[wave], prod[wave]);
-        if (lane == 0) P.out[(size_t)g * CS + k] = q;
-    }
-}
 
 // =============================================================================================
 // Fused encode + Exp-Golomb, K1 (dct3d_encode_eg_dev; encoder.c:206-274 up to the deflate)
@@ -479,7 +449,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
 // Launchers
 // =============================================================================================
 // Encode: 8x8x8 = encode16_kernel (16 lanes per cube, in-wave exact replay, one launch per call);
-// 8x8x4 = encode_kernel<4> (8 lanes per cube, flag list + encode_fixup_kernel).  Both store the int32
+// 8x8x4 = encode_kernel<4> (8 lanes per cube, in-wave exact replay, one launch).  Both store the int32
 // output non-temporally.  The variants that lost (8 lanes per cube at 8x8x8, plain stores, NT loads,
 // LDS-padded occupancy) are recorded in profiles/r01/encode_variant_sweep.txt, not built.
 namespace {
@@ -490,8 +460,6 @@ void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, hipStream_t 
     hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
 }
 }  // namespace
-
-bool encode_replays_inwave(int D) { return D == 8; }
 
 int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
@@ -511,12 +479,6 @@ int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipSt
     if (P.n_cubes == 0) return 0;
     if (D == 8) launch_enc_eg_t<8>(P, E, st);
     else launch_enc_eg_t<4>(P, E, st);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-int launch_encode_fixup(int D, const FixupParams& P, int grid, hipStream_t st) {
-    if (D != 4) return -1;  // 8x8x8 replays inside encode16_kernel
-    hipLaunchKernelGGL(encode_fixup_kernel<4>, dim3(grid), dim3(256), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

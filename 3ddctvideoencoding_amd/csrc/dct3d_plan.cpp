@@ -7,7 +7,7 @@
 //    in HashMap iteration order (DCT.java:98).  S_g are sums of integer pixels, exact in double, so
 //    the Java result is fully determined by (group membership, group coefficient bits, fold order).
 //    This file re-derives all three with a Java 8 HashMap emulation; the device exact-fold path
-//    (fixup kernel) replays that fold bit for bit.
+//    (the kernels' in-wave replays) repeats that fold bit for bit.
 // 2. Certification bounds: the fp32 fused encoder is analysed by running the kernel's own
 //    butterflies (dct_butterfly.h) on a Tracked value type that carries the exact linear functional
 //    and a rigorous rounding-error bound.  Any coefficient whose fp32 quotient lies within the bound
@@ -417,6 +417,9 @@ bool build_plan(int cw, int ch, int cd, Plan& p) {
                     if (p.fwd_group_of[(size_t)k * cs + n] == 0xFF) p.enc_dev[k] += std::fabs(own[n]);
             }
     if (p.fwd_ngroups[0] != 1) return false;  // the kernels take the DC as one exact product
+    if (cd == 4)  // the 8x8x4 encode's in-wave fold keeps kMaxGroups4 sums per cube (40 needed)
+        for (int k = 0; k < cs; k++)
+            if (p.fwd_ngroups[k] > kMaxGroups4) return false;
     p.coef_dc = p.fwd_coef[0];
 
     // ---- inverse coefficient matrix (InverseDCT.initialize) ----

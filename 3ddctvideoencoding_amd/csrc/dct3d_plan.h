@@ -8,6 +8,7 @@
 namespace dct3d {
 
 constexpr int kMaxGroups = 64;   // per-coefficient group slots in the device fold table
+constexpr int kMaxGroups4 = 48;  // 8x8x4: group sums per cube of the encode's in-wave fold (kGM4Dev)
 constexpr int kMaxS = 32;        // s = kx + ky + kz table size (max 21 for 8x8x8)
 
 struct Plan {

@@ -54,25 +54,22 @@ struct dct3d_ctx {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     bool profiling = false;
-    // ring of event quadruples (main begin/end, fixup begin/end); resolved lazily
+    // ring of event quadruples (main kernel begin/end, auxiliary launch begin/end); resolved lazily
     static constexpr int kRing = 256;
     hipEvent_t ev[kRing][4] = {};
     int ring_head = 0, ring_pending = 0;
     uint64_t n_timed = 0;
-    double kernel_ms = 0.0, fixup_ms = 0.0;
+    double kernel_ms = 0.0, aux_ms = 0.0;
     // plan tables on device
     DevBuf d_ngroups, d_coef, d_group_of, d_inv_coef, d_tabs, d_tabs64;
     // test / diagnostic options (dct3d_ctx_set_option): how later calls reach their results
-    uint32_t opt_flag_cap = 0;      // 0: default capacity
     double opt_dec_margin = 0.0;    // added to the decode margin
     bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
     // certify-or-replay state
-    DevBuf d_flags, d_cubes, d_counters;
-    uint32_t flag_cap = 0;
     uint64_t last_units = 0;
     bool last_valid = false;
-    // in-wave replay (8x8x8 encode): two counter slots that alternate between calls; each launch zeroes
+    // in-wave replay (encode, decode): two counter slots that alternate between calls; each launch zeroes
     // the other slot for the next call, so a call needs no reset copy (zeroed once at creation).
     // Slot j (2 kCountSpread words at j * 2 kCountSpread): Java-fold replays, then second-certificate
     // settlements, each spread over kCountSpread words (dct3d_kernels.h).
@@ -219,7 +216,6 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         memcpy(t64 + 64, p.enc_thr64, sizeof(p.enc_thr64));
         rc = upload(c->d_tabs64, t64, sizeof(t64));
     }
-    if (!rc) rc = c->d_counters.grow(16);
     if (!rc) rc = c->d_enc_counts.grow(4 * kCountSpread * sizeof(uint32_t));
     if (!rc && hipMemset(c->d_enc_counts.p, 0, 4 * kCountSpread * sizeof(uint32_t)) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc) {
@@ -241,8 +237,8 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->own_stream) (void)hipStreamSynchronize(c->own_stream);
-    for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_tabs64, &c->d_flags,
-                      &c->d_cubes, &c->d_counters, &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
+    for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_tabs64,
+                      &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egf_slot,
                       &c->d_egf_lbits})
@@ -277,10 +273,6 @@ int dct3d_ctx_info(const dct3d_ctx* c, int* device, int* block_d, void** hip_str
 int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
     if (!c || !(value >= 0.0)) return DCT3D_EINVAL;
     switch (option) {
-        case DCT3D_OPT_FLAG_CAP:
-            if (value > 4294967295.0) return DCT3D_EINVAL;
-            c->opt_flag_cap = (uint32_t)value;
-            return DCT3D_OK;
         case DCT3D_OPT_DEC_MARGIN: c->opt_dec_margin = value; return DCT3D_OK;
         case DCT3D_OPT_ENC_NO_RECHECK: c->opt_enc_no_recheck = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
@@ -311,7 +303,7 @@ static int resolve_timers(dct3d_ctx* c, int n) {
         if (hipEventElapsedTime(&a, e[0], e[1]) != hipSuccess || hipEventElapsedTime(&b, e[2], e[3]) != hipSuccess)
             return DCT3D_EDEVICE;
         c->kernel_ms += a;
-        c->fixup_ms += b;
+        c->aux_ms += b;
         c->n_timed++;
         c->ring_pending--;
     }
@@ -333,7 +325,7 @@ int dct3d_reset_timers(dct3d_ctx* c) {
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     int rc = resolve_timers(c, dct3d_ctx::kRing);
     c->n_timed = 0;
-    c->kernel_ms = c->fixup_ms = 0.0;
+    c->kernel_ms = c->aux_ms = 0.0;
     return rc;
 }
 
@@ -344,27 +336,19 @@ int dct3d_get_stats(dct3d_ctx* c, dct3d_stats* st) {
     if (resolve_timers(c, dct3d_ctx::kRing)) return DCT3D_EDEVICE;
     st->n_timed = c->n_timed;
     st->kernel_ms_total = c->kernel_ms;
-    st->fixup_ms_total = c->fixup_ms;
+    st->aux_ms_total = c->aux_ms;
     st->n_units = c->last_units;
-    if (!c->last_valid) return DCT3D_OK;
-    uint32_t cnt[4] = {0, 0, 0, 0};
-    if (c->last_count_slot >= 0) {  // in-wave replay: the call's slot; no overflow path exists
-        std::vector<uint32_t> w(2 * kCountSpread);
-        if (hipMemcpyAsync(w.data(), (uint32_t*)c->d_enc_counts.p + c->last_count_slot * 2 * kCountSpread,
-                           w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipStreamSynchronize(c->stream) != hipSuccess)
-            return DCT3D_EDEVICE;
-        for (int i = 0; i < kCountSpread; i++) {
-            st->n_flagged += w[i];
-            st->n_rechecked += w[kCountSpread + i];
-        }
-        return DCT3D_OK;
-    } else if (hipMemcpyAsync(cnt, c->d_counters.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+    if (!c->last_valid || c->last_count_slot < 0) return DCT3D_OK;
+    // the call's counter slot (in-wave replays: every replaying path has one)
+    std::vector<uint32_t> w(2 * kCountSpread);
+    if (hipMemcpyAsync(w.data(), (uint32_t*)c->d_enc_counts.p + c->last_count_slot * 2 * kCountSpread,
+                       w.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
+    for (int i = 0; i < kCountSpread; i++) {
+        st->n_flagged += w[i];
+        st->n_rechecked += w[kCountSpread + i];
     }
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    st->n_flagged = cnt[0];
-    st->n_overflow_cubes = cnt[1];
     return DCT3D_OK;
 }
 
@@ -376,21 +360,6 @@ static int check_geometry(const dct3d_ctx* c, int w, int h, int n_stacks, uint64
     const uint64_t n = cps * (uint64_t)n_stacks;
     if (n >= (1ull << 31) / 8) return DCT3D_EINVAL;   // 32-bit cube indices in the kernels
     *n_cubes = n;
-    return DCT3D_OK;
-}
-
-static int ensure_flag_buffers(dct3d_ctx* c, uint64_t n_cubes) {
-    // flag list: generous (1/64 of all units); overflow degrades to whole-cube replay, never to
-    // wrong results.  cube list: one entry per cube at most.
-    uint64_t cap = n_cubes * (uint64_t)c->plan.cs / 64 + 4096;
-    if (cap > 0xFFFFFFF0ull) cap = 0xFFFFFFF0ull;
-    // test option: shrink the list to exercise the whole-cube replay path (tests/test_gpu_parity.py)
-    if (c->opt_flag_cap && c->opt_flag_cap < cap) cap = c->opt_flag_cap;
-    int rc = c->d_flags.grow(cap * sizeof(unsigned long long));
-    if (rc) return rc;
-    rc = c->d_cubes.grow((n_cubes + 1) * sizeof(uint32_t));
-    if (rc) return rc;
-    c->flag_cap = (uint32_t)cap;
     return DCT3D_OK;
 }
 
@@ -430,13 +399,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     c->last_count_slot = -1;
     if (n_cubes == 0) return DCT3D_OK;
     const int D = c->bd;
-    // 8x8x8: one launch, uncertified coefficients replayed inside the wave; 8x8x4: flag list + fixup
-    const bool inwave = encode_replays_inwave(D);
-    if (!inwave) {
-        rc = ensure_flag_buffers(c, n_cubes);
-        if (rc) return rc;
-        if (hipMemsetAsync(c->d_counters.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    }
+    // one launch: uncertified coefficients are replayed inside the wave (exact Java fold)
     const uint64_t plane = (uint64_t)w * h;
     EncodeParams P;
     memset(&P, 0, sizeof(P));
@@ -455,53 +418,23 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.tab_rstep = tabs;
     P.tab_G = tabs + kMaxS;
     P.tab_E = tabs + 2 * kMaxS;
-    P.flag_list = (unsigned long long*)c->d_flags.p;
-    P.counters = (unsigned int*)c->d_counters.p;
-    P.flag_cap = c->flag_cap;
-    P.cube_list = (uint32_t*)c->d_cubes.p;
     P.ngroups = (const int32_t*)c->d_ngroups.p;
     P.coef = (const double*)c->d_coef.p;
     P.group_of = (const uint8_t*)c->d_group_of.p;
-    if (inwave) {
-        P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
-        P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
-        P.tab64 = (const double*)c->d_tabs64.p;
-        P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
-    }
+    P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
+    P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+    P.tab64 = (const double*)c->d_tabs64.p;
+    P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (launch_encode(D, P, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[1], c->stream);
-    if (inwave) {
-        if (ev) {  // no fixup launch: the second event pair brackets nothing
-            (void)hipEventRecord(ev[2], c->stream);
-            (void)hipEventRecord(ev[3], c->stream);
-        }
-        c->last_count_slot = c->enc_slot;
-        c->enc_slot ^= 1;
-        c->last_units = n_cubes * (uint64_t)c->plan.cs;
-        c->last_valid = true;
-        if (d_dct) return forward_f64_raster(c, d_raster, w, h, n_cubes, d_dct);
-        return DCT3D_OK;
+    if (ev) {  // single launch: the second event pair brackets nothing
+        (void)hipEventRecord(ev[1], c->stream);
+        (void)hipEventRecord(ev[2], c->stream);
+        (void)hipEventRecord(ev[3], c->stream);
     }
-    FixupParams F;
-    F.raster = d_raster;
-    F.out = d_q;
-    F.cubes_per_stack = P.cubes_per_stack;
-    F.nbx = P.nbx;
-    F.width = P.width;
-    F.plane = P.plane;
-    F.stack_stride = P.stack_stride;
-    F.flag_list = P.flag_list;
-    F.counters = P.counters;
-    F.flag_cap = P.flag_cap;
-    F.cube_list = P.cube_list;
-    F.ngroups = (const int32_t*)c->d_ngroups.p;
-    F.coef = (const double*)c->d_coef.p;
-    F.group_of = (const uint8_t*)c->d_group_of.p;
-    if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_encode_fixup(D, F, 1024, c->stream)) return DCT3D_EKERNEL;
-    if (ev) (void)hipEventRecord(ev[3], c->stream);
+    c->last_count_slot = c->enc_slot;
+    c->enc_slot ^= 1;
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     c->last_valid = true;
     if (d_dct) return forward_f64_raster(c, d_raster, w, h, n_cubes, d_dct);
@@ -701,7 +634,7 @@ int dct3d_decode_stacks(dct3d_ctx* c, const int32_t* q, int w, int h, int n_stac
 }
 
 // ---- drop-in (A): float cube-major <-> float cube-major --------------------------------------
-// one launch of the float kernel, timed like the fused kernels when profiling is on (no fixup:
+// one launch of the float kernel, timed like the fused kernels when profiling is on (no auxiliary launch:
 // the second event pair brackets nothing)
 static int cube_f32_dev(dct3d_ctx* c, const float* d_in, size_t n_cubes, float* d_out, bool inverse) {
     if (!c || (n_cubes && (!d_in || !d_out)) || n_cubes >= (1ull << 31) / 8) return DCT3D_EINVAL;
@@ -1039,7 +972,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
 }
 
 // Fused stream -> raster decode of stacks [st0, st0 + ns) after eg_decode_front: the decode kernel parses
-// its cubes at the marks (no int32 cube-major intermediate), the fixup replays flagged cubes by
+// its cubes at the marks (no int32 cube-major intermediate) and replays uncertified cubes in the wave by
 // re-parsing them.  out_stack0 = where stack st0 goes (the raster pointer is rebased so that the
 // kernels' global cube indices land in it).
 }  // extern "C"

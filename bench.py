@@ -180,7 +180,7 @@ def pmc_traffic(config: str, kernel: str, depth: int):
     vals = {}
     for r in csv.DictReader(open(path)):
         name = r["kernel"]
-        if (f"{kernel}<{depth}" in name or (kernel == "encode16_kernel" and f"{kernel}<" in name)) and "fixup" not in name:
+        if (f"{kernel}<{depth}" in name or (kernel == "encode16_kernel" and f"{kernel}<" in name)):
             vals[r["counter"]] = float(r["avg_per_launch_raw"])
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None, None
@@ -448,7 +448,7 @@ def main():
     if fused_dec:  # the cube's share of the stream in, u8 out
         bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes)
     kernel_ms = st["kernel_ms_total"] / max(1, st["n_timed"])
-    fixup_ms = st["fixup_ms_total"] / max(1, st["n_timed"])
+    aux_ms = st["aux_ms_total"] / max(1, st["n_timed"])
     alg_bytes = n_cubes * bytes_per_cube
     achieved = alg_bytes / (dev_step_ms * 1e-3) / 1e9 if n_cubes else 0.0       # step basis
     kernel_achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
@@ -461,8 +461,7 @@ def main():
         "encode_eg_kernel" if fused else ("encode16_kernel" if depth == 8 else "encode_kernel"))
     if direction in ("forward_f32", "inverse_f32"):
         kname = "cube_f32_kernel"
-    step_kernels = {"encode": [kname] if depth == 8 else ["memset (counter reset)", kname, "encode_fixup_kernel"],
-                    "decode": ["memset (counter reset)", kname, "decode_fixup_kernel"]}.get(direction, [kname])
+    step_kernels = [kname] + (["eg_compact_kernel"] if fused else [])
     traffic, traffic_src = pmc_traffic(a.config, kname, depth) if not (a.stacks or a.job_stacks) else (None, None)
 
     # per-rank record (strong scaling: shards differ in size; the job rate is total cubes / max time)
@@ -524,7 +523,7 @@ def main():
             "device_ms_per_step": dev_step_ms,
             "kernel": kname,
             "kernel_ms": kernel_ms,
-            "fixup_ms": fixup_ms,
+            "aux_ms": aux_ms,
             "kernel_only_achieved": kernel_achieved,
             "kernel_only_frac": kernel_achieved / HBM_PEAK_GBS,
         },
@@ -535,7 +534,7 @@ def main():
         "mcubes_per_s_per_gpu": value / world / 1e6,
         "eg_stage": None if direction not in ("encode_eg", "decode_eg") else {
             "path": ("fused" if fused_dec else "two-step") if direction == "decode_eg" else ("fused" if fused else "two-step"),
-            "ms_per_step": (fixup_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
+            "ms_per_step": (aux_ms if fused else sum(x.elapsed_time(y) for x, y in eg_ev[-a.steps:]) / a.steps),
             "bits_per_value": eg_info["bits"] / (max(1, n_cubes) * cs),
             "stream_bytes_per_step": (eg_info["bits"] + 7) // 8},
         "round_trip": round_trip,

@@ -60,7 +60,7 @@ extern "C" {
 #define DCT3D_ENOSPC 5      /* an output buffer is too small (nothing was written past its end) */
 #define DCT3D_ENODATA 6     /* an input stream ends before the requested data is complete */
 
-#define DCT3D_ABI_VERSION 7
+#define DCT3D_ABI_VERSION 8
 
 typedef struct dct3d_ctx dct3d_ctx;
 
@@ -69,11 +69,11 @@ typedef struct {
     uint64_t n_units;          /* coefficients (encode) or pixels (decode) produced by the last call */
     uint64_t n_flagged;        /* units of the last call re-done by the exact Java fold (decode: the 32
                                   pixels of every lane with an uncertified pixel) */
-    uint64_t n_overflow_cubes; /* 8x8x4 encode: cubes of the last call re-done whole (flag list full) */
     /* HIP-event timing of every encode/decode call since dct3d_reset_timers (profiling on) */
     uint64_t n_timed;          /* calls timed */
     double kernel_ms_total;    /* main transform kernel, summed */
-    double fixup_ms_total;     /* exact-fold kernel (8x8x4 encode), summed; 0 for single-launch calls */
+    double aux_ms_total;       /* the call's auxiliary launch, summed (fused Exp-Golomb encode: the
+                                  compaction kernel); 0 for single-launch calls */
     uint64_t n_rechecked;      /* 8x8x8 encode: units of the last call the fp32 certificate left open
                                   and the fp64 second certificate settled (not counted in n_flagged) */
 } dct3d_stats;
@@ -122,8 +122,6 @@ int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_s
 /* Test / diagnostic options of a ctx.  Each one changes only HOW later calls reach their results
  * (the results stay bit-identical): tests use them to drive the rare paths.  value 0 restores the
  * default.  Unknown options: DCT3D_EINVAL. */
-#define DCT3D_OPT_FLAG_CAP 1          /* flag-list capacity in entries (8x8x4 encode): overflow sends cubes
-                                         to the whole-cube replay */
 #define DCT3D_OPT_DEC_MARGIN 2        /* added to the decode certification margin: lanes go to the in-wave
                                          exact replay */
 #define DCT3D_OPT_ENC_NO_RECHECK 3    /* 1: the 8x8x8 encode skips its fp64 second certificate, so every

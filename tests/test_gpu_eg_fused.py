@@ -90,7 +90,7 @@ def test_fused_carry_partial_byte(pkg, oracle, plan8, gpu_ctx8, carry_bits):
 @pytest.mark.parametrize("kind", ["ramp", "uniform"])
 def test_fused_1080p_matches_two_step(pkg, gpu_ctx8, gpu_ctx4, depth, kind):
     """1080p, 2 stacks: uncertified coefficients (uniform content, 8x8x4 exact ties) replayed inside
-    the fused kernel must give the fixup kernel's values"""
+    the fused kernel must give the stand-alone encode kernel's values"""
     ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
     fr = pkg.synthetic.frames(1920, 1080, 2 * depth, kind=kind)
     q = ctx.encode_stacks(fr)

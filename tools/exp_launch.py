@@ -8,7 +8,7 @@ s = torch.cuda.Stream(); torch.cuda.set_stream(s); ctx.set_stream(s.cuda_stream)
 fr = torch.zeros((8, 8, 64), dtype=torch.uint8, device="cuda")
 q = torch.zeros(8 * 8 * 64, dtype=torch.int32, device="cuda")
 out = torch.empty_like(fr)
-for _ in range(20):                      # tiny decode + fixup, tiny encode + fixup
+for _ in range(20):                      # tiny decode, tiny encode
     ctx.decode_stacks_dev(q, 64, 8, 1, out)
     ctx.encode_stacks_dev(fr, 64, 8, 1, q)
 buf = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
