@@ -168,48 +168,50 @@ struct WinReader {
 };
 
 // A validated stream in an LDS window (the consumers after the mark pass): no bounds checks (a valid
-// parse stays inside the staged range, which carries 4 words of slack), the leading-zero count from the
-// top 32 bits (a valid code has < 32 leading zeros, and >= 33 bits are buffered after a refill).
+// parse stays inside the staged range, which carries 4 words of slack).  The buffer is two 32-bit words
+// hi:lo, left-aligned, its top `avail` bits valid and the rest zero; the position is implied
+// (next * 32 - avail), so a code costs a leading-zero count, one funnel shift (v_alignbit_b32) and one
+// shift instead of the 64-bit shifts and position update of a 64-bit buffer.  A refill appends the word
+// `pre` whenever fewer than 32 bits are buffered, so a code of up to 31 bits (|v| < 2^15: every code an
+// encoder of 8-bit frames writes) is always whole in hi:lo; a longer one is re-read at its absolute
+// position after a wave-uniform test.
 struct ValidWinReader {
     const uint32_t* s;
-    uint32_t next;
-    uint64_t buf;
-    int avail;
-    uint32_t pos;
+    uint32_t next;   // index of the word held in `pre`; the buffer ends at bit next * 32
+    uint32_t hi, lo;
+    uint32_t avail;
     uint32_t pre;
     __device__ __forceinline__ void seek(uint32_t p) {
-        pos = p;
         const uint32_t k = p >> 5;
-        const int sh = (int)(p & 31);
-        buf = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
-        avail = 64 - sh;
+        const uint64_t b = (((uint64_t)s[k] << 32) | s[k + 1]) << (p & 31);
+        hi = (uint32_t)(b >> 32);
+        lo = (uint32_t)b;
+        avail = 64u - (p & 31);
         next = k + 2;
         pre = s[next];
     }
     __device__ __forceinline__ uint32_t get() {
-        if (avail <= 32) {
-            buf |= (uint64_t)pre << (32 - avail);
-            avail += 32;
+        if (avail < 32u) {  // hi holds the avail valid bits, lo is zero: pre goes right behind them
+            hi |= pre >> avail;
+            lo = __builtin_amdgcn_alignbit(pre, 0u, avail);  // pre << (32 - avail); 0 for avail = 0
+            avail += 32u;
             pre = s[++next];
         }
-        const int z = __builtin_clz((uint32_t)(buf >> 32));  // a valid code: the top 32 bits are not 0
-        const int width = 2 * z + 1;
-        const bool fits = width <= avail;
-        // the common case for every lane without a branch; a code longer than the buffered bits
-        // (|v| >= 2^16) is re-read after a wave-uniform test (no divergent if / else per code)
-        uint32_t code = (uint32_t)(buf >> (64 - width));
-        buf <<= width;
-        avail -= width;
-        pos += (uint32_t)width;
-        if (__builtin_expect(__ballot(!fits) != 0ull, 0)) {
-            if (!fits) {
-                const uint32_t p = pos - (uint32_t)width;
+        const uint32_t z = __builtin_clz(hi);  // a valid code: hi (>= 32 buffered bits) is not 0
+        const uint32_t w = 2u * z + 1u;
+        uint32_t code = hi >> (32u - w);  // w <= 31 (z < 16); else garbage, replaced below
+        hi = __builtin_amdgcn_alignbit(hi, lo, 32u - w);
+        lo <<= w;
+        avail -= w;
+        if (__builtin_expect(__ballot(z >= 16u) != 0ull, 0)) {
+            if (z >= 16u) {  // a code of 33+ bits: read at its absolute position
+                const uint32_t p = next * 32u - (avail + w);
                 const uint32_t k = p >> 5;
                 const int sh = (int)(p & 31);
-                const uint64_t hi = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
-                const uint64_t w = sh ? (hi | ((uint64_t)s[k + 2] >> (32 - sh))) : hi;
-                code = (uint32_t)(w >> (64 - width));
-                seek(pos);
+                const uint64_t h = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
+                const uint64_t x = sh ? (h | ((uint64_t)s[k + 2] >> (32 - sh))) : h;
+                code = (uint32_t)(x >> (64 - w));
+                seek(p + w);
             }
         }
         return code;
