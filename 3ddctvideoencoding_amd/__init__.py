@@ -44,7 +44,7 @@ ABI_SYMBOLS = (
 )
 # Every symbol include/dct3d_diag.h declares (libdct3d_diag.so; none of them is in libdct3d.so).
 DIAG_SYMBOLS = ("dct3d_fill_synthetic_dev", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
-                "dct3d_decode_diag_dev")
+                "dct3d_encode_diag_dev", "dct3d_decode_diag_dev")
 
 
 class Dct3dError(RuntimeError):
@@ -134,6 +134,7 @@ def diag_lib() -> C.CDLL:
         D.dct3d_fill_synthetic_dev.argtypes = [vp, vp, i32, i32, i32, u64, i64, i32]
         D.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
         D.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
+        D.dct3d_encode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
         D.dct3d_decode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
         _diag = D
     return _diag
@@ -313,6 +314,11 @@ class Context:
         """Diagnostic: the encode's memory traffic without its compute (d_q is NOT a DCT)."""
         _check(diag_lib().dct3d_encode_memonly_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q)),
                "dct3d_encode_memonly_dev")
+
+    def encode_diag_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q, mode: int) -> None:
+        """Diagnostic: the encode's memory part (mode 1) or, 8x8x8, its compute part (mode 2) alone."""
+        _check(diag_lib().dct3d_encode_diag_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q), mode),
+               "dct3d_encode_diag_dev")
 
     def decode_diag_dev(self, d_q, width: int, height: int, n_stacks: int, d_frames, mode: int) -> None:
         """Diagnostic: the 8x8x8 decode's memory part (mode 1) or compute part (mode 2) alone."""

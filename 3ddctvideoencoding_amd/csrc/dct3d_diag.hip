@@ -11,6 +11,7 @@
 // The twins instantiate the product's own device templates (dct3d_encode_dev.h, dct3d_decode_dev.h)
 // with the transform switched off, so their memory behaviour is the product's.  C-ABI:
 // include/dct3d_diag.h.
+#include <cmath>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -246,6 +247,54 @@ void* scratch(int device, size_t bytes) {
     return s.p;
 }
 
+// The 8x8x8 encode's tables on the device for the compute-only twin (its certificate, second
+// certificate and Java fold tables, from dct3d_plan_query; the second certificate's basis from the cosine
+// directly: the twin's output is discarded, only its work matters).  Built once per device.
+constexpr int kMaxS = 32;  // the plan's per-s table size (dct3d_plan.h, dct3d_plan_info)
+struct EncTables {
+    float* tabs = nullptr;  // [3 * kMaxS] 1/step, G, E
+    double* tab64 = nullptr;
+    int32_t* ngroups = nullptr;
+    double* coef = nullptr;
+    uint8_t* group_of = nullptr;
+    double coef_dc = 0.0;
+};
+EncTables g_enc8[64];
+const EncTables* enc8_tables(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (device < 0 || device >= 64) return nullptr;
+    EncTables& t = g_enc8[device];
+    if (t.tabs) return &t;
+    constexpr int CS = 512;
+    dct3d_plan_info info;
+    std::vector<int32_t> ng(CS);
+    std::vector<double> cf((size_t)CS * kMaxGroupsDev);
+    std::vector<uint8_t> go((size_t)CS * CS);
+    if (dct3d_plan_query(8, 8, 8, &info, ng.data(), cf.data(), go.data(), nullptr) != DCT3D_OK) return nullptr;
+    float tabs[3 * kMaxS];
+    memcpy(tabs, info.enc_rstep, sizeof(float) * kMaxS);
+    memcpy(tabs + kMaxS, info.enc_G, sizeof(float) * kMaxS);
+    memcpy(tabs + 2 * kMaxS, info.enc_E, sizeof(float) * kMaxS);
+    double t64[64 + kMaxS];
+    for (int kk = 0; kk < 8; kk++)
+        for (int n = 0; n < 8; n++)
+            t64[kk * 8 + n] = (kk ? 0.5 : std::sqrt(0.125)) * std::cos((2 * n + 1) * kk * 3.14159265358979323846 / 16);
+    memcpy(t64 + 64, info.enc_thr64, sizeof(double) * kMaxS);
+    EncTables n;
+    if (hipMalloc((void**)&n.tabs, sizeof(tabs)) != hipSuccess || hipMalloc((void**)&n.tab64, sizeof(t64)) != hipSuccess ||
+        hipMalloc((void**)&n.ngroups, ng.size() * 4) != hipSuccess || hipMalloc((void**)&n.coef, cf.size() * 8) != hipSuccess ||
+        hipMalloc((void**)&n.group_of, go.size()) != hipSuccess ||
+        hipMemcpy(n.tabs, tabs, sizeof(tabs), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(n.tab64, t64, sizeof(t64), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(n.ngroups, ng.data(), ng.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(n.coef, cf.data(), cf.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(n.group_of, go.data(), go.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return nullptr;
+    n.coef_dc = info.coef_dc;
+    t = n;
+    return &t;
+}
+
 }  // namespace
 }  // namespace dct3d
 
@@ -278,11 +327,16 @@ int dct3d_bandwidth_probe_dev(dct3d_ctx* c, const uint8_t* d_in, void* d_out, si
 }
 
 int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q) {
+    return dct3d_encode_diag_dev(c, d_raster, w, h, n_stacks, d_q, 1);
+}
+
+int dct3d_encode_diag_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode) {
     CtxView v;
     if ((!d_raster || !d_q) && n_stacks) return DCT3D_EINVAL;
     int rc = view(c, v);
     uint64_t n_cubes = 0;
     if (rc || (rc = geometry(w, h, n_stacks, &n_cubes))) return rc;
+    if (mode != 1 && !(mode == 2 && v.bd == 8)) return DCT3D_EINVAL;
     if (n_cubes == 0) return DCT3D_OK;
     EncodeParams P;
     memset(&P, 0, sizeof(P));
@@ -296,10 +350,25 @@ int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
     P.stack_stride = P.plane * v.bd;
-    if (v.bd == 8) {  // the twin of encode16_kernel
+    if (v.bd == 8) {  // the twins of encode16_kernel
         const uint32_t groups = (P.n_cubes + kE16CPW - 1) / kE16CPW;
-        hipLaunchKernelGGL((encode16_kernel<true, true>), dim3((groups + kWavesPerBlock - 1) / kWavesPerBlock),
-                           dim3(kBlock), 0, v.stream, P);
+        const dim3 grid((groups + kWavesPerBlock - 1) / kWavesPerBlock);
+        if (mode == 1) {
+            hipLaunchKernelGGL((encode16_kernel<true, 1>), grid, dim3(kBlock), 0, v.stream, P);
+        } else {  // compute only, with the product's tables
+            const EncTables* t = enc8_tables(v.device);
+            if (!t) return DCT3D_ENOMEM;
+            P.coef_dc = t->coef_dc;
+            P.tab_rstep = t->tabs;
+            P.tab_G = t->tabs + kMaxS;
+            P.tab_E = t->tabs + 2 * kMaxS;
+            P.tab64 = t->tab64;
+            P.recheck = 1u;
+            P.ngroups = t->ngroups;
+            P.coef = t->coef;
+            P.group_of = t->group_of;
+            hipLaunchKernelGGL((encode16_kernel<true, 2>), grid, dim3(kBlock), 0, v.stream, P);
+        }
     } else {
         const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
         hipLaunchKernelGGL((encode_memonly_kernel<4>), dim3((groups + kWavesPerBlock - 1) / kWavesPerBlock),

@@ -776,16 +776,20 @@ __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2
     wave_lds_sync();
 }
 
-// MEM (dct3d_encode_memonly_dev, DIAGNOSTIC: the output is NOT a DCT): the same loads, staging and
-// stores with the transform, quantisation and certification replaced by a few integer ops.
+// MODE 1 (dct3d_encode_diag_dev memory only, DIAGNOSTIC: the output is NOT a DCT): the same loads,
+// staging and stores with the transform, quantisation and certification replaced by a few integer ops.
+// MODE 2 (compute only, DIAGNOSTIC): ramp-like rows made from the lane and cube indices instead of the
+// loads, the whole transform / quantise / certify / staging, the stores suppressed by a runtime
+// condition (P.width == 0 never holds), so its time is the kernel's issue work alone.
 // One launch is the whole encode: no flag list, no counter reset, no fixup launch.  Block 0 zeroes the
 // next call's counter slot (P.replay_clear; the two slots alternate between calls).  7 waves per SIMD
 // (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (they
 // spill a few registers to scratch instead, off the main path).
 static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the wave's region");
-template <bool NT, bool MEM = false>
+template <bool NT, int MODE = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
+    constexpr bool MEM = MODE == 1, COMP = MODE == 2;
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
     __shared__ float4 s_tab[kTabN];
     __shared__ double s_b64[96];  // second certificate tables (rare path)
@@ -796,8 +800,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     const uint32_t g = cube0 + c;
     const bool valid = g < P.n_cubes;
     uint2 raw[4];
-    e16_load(P, g, valid, k, h, raw);
-    if (!MEM && blockIdx.x == 0 && P.replay_clear) {
+    if constexpr (COMP) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint32_t b0 = 96u + 5u * (uint32_t)k + 7u * (uint32_t)(4 * h + r) + (g & 15u);
+            raw[r] = make_uint2((b0 * 0x01010101u) + 0x09060300u, (b0 * 0x01010101u) + 0x15120F0Cu);
+        }
+    } else {
+        e16_load(P, g, valid, k, h, raw);
+    }
+    if (!MEM && !COMP && blockIdx.x == 0 && P.replay_clear) {
 #pragma unroll
         for (int i = 0; i < 2 * kCountSpread / kBlock; i++) P.replay_clear[i * kBlock + threadIdx.x] = 0u;
     }
@@ -844,7 +856,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         for (int t = 0; t < 4; t++) {
             const int q = t * 64 + lane;  // 16-byte chunk of the round's two cubes
             const int cc = q >> 7, face = (q >> 4) & 7, w = q & 15;
-            if (rcube0 + cc < P.n_cubes) {
+            if (rcube0 + cc < P.n_cubes && (!COMP || P.width == 0u)) {
                 const int4 v = *(const int4*)(wl + cc * kE16SC + face * kFace + w * 16);
                 store16<NT>(outb + (size_t)q * 16, v);
             }

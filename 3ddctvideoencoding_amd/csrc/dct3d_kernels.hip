@@ -466,7 +466,7 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     if (D == 8) {
         const uint32_t groups = (P.n_cubes - P.g_base + kE16CPW - 1) / kE16CPW;
         const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-        hipLaunchKernelGGL((encode16_kernel<true, false>), dim3(blocks), dim3(kBlock), 0, st, P);
+        hipLaunchKernelGGL((encode16_kernel<true, 0>), dim3(blocks), dim3(kBlock), 0, st, P);
     } else {
         const uint32_t groups = (P.n_cubes - P.g_base + kCubesPerWave - 1) / kCubesPerWave;
         const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;

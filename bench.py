@@ -226,6 +226,8 @@ def measure_ceiling(ctx, torch, frames, q, reps, geom=None, dec_geom=None):
         n_cubes = q.numel() // (bpc // 5)
         out["encode_memonly_ms"] = ms
         out["encode_memonly_GBs"] = n_cubes * bpc / (ms * 1e-3) / 1e9
+        if bpc == 5 * 512:  # 8x8x8: the compute part alone (no loads, no stores)
+            out["encode_computeonly_ms"] = timed(lambda: ctx.encode_diag_dev(frames, width, height, stacks, q, 2))
     for name, mode, bytes_per_px in (("mix_1r4w", 0, 5), ("copy", 1, 2), ("write", 2, 4), ("write_plain", 5, 4),
                                       ("read", 3, 1)):
         ctx.bandwidth_probe_dev(frames, q, n_px, mode)

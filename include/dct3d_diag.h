@@ -32,6 +32,11 @@ int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, 
  * reaches on this device. */
 int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                              int32_t *d_q);
+/* The encode kernel split in two (bench support; d_q receives NOT a DCT): mode 1 = memory only (as
+ * dct3d_encode_memonly_dev), mode 2 = compute only (8x8x8 contexts: rows made from the lane and cube
+ * indices instead of the loads, the whole transform / quantise / certify / staging, no stores). */
+int dct3d_encode_diag_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
+                          int32_t *d_q, int mode);
 
 /* The 8x8x8 decode kernel split in two (bench support; d_raster receives NOT a decode): mode 1 = memory
  * only (the same staged loads and raster stores, no transform), mode 2 = compute only (no global loads,
