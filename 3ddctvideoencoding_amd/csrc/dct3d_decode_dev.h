@@ -484,6 +484,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         }
         if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
     }
+    __builtin_amdgcn_s_setprio(2);  // the store phase ahead of the computing waves (as encode16_kernel)
     dec_store_tile<D>(P, wl, lane, cube0, outw, valid);
 }
 
@@ -503,7 +504,9 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     char* wl = lds + wave * kDecWaveLds;
     const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * DecGeom<D>::CPW;
     int4 v[8];
+    __builtin_amdgcn_s_setprio(3);  // a starting wave issues its loads ahead of the computing ones
     dec_load_tile<D>(P, cube0, lane, v);
+    __builtin_amdgcn_s_setprio(0);
     dec_clear_next_slot(P);
     dec_stage_tile<D>(wl, lane, v);
     wave_lds_sync();
