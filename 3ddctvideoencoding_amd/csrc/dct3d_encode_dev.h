@@ -807,9 +807,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
             raw[r] = make_uint2((b0 * 0x01010101u) + 0x09060300u, (b0 * 0x01010101u) + 0x15120F0Cu);
         }
     } else {
-        __builtin_amdgcn_s_setprio(3);  // a starting wave issues its loads ahead of the computing ones
+        // a starting wave computes its addresses and issues its loads at the top priority: under the
+        // default oldest-first issue they queue behind the computing waves' VALU work, and a box whose
+        // encode loses the overlap of memory and compute that way runs 10 % slower (variant_sweep.txt)
+        if constexpr (!MEM) __builtin_amdgcn_s_setprio(3);
         e16_load(P, g, valid, k, h, raw);
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (!MEM) __builtin_amdgcn_s_setprio(0);
     }
     if (!MEM && !COMP && blockIdx.x == 0 && P.replay_clear) {
 #pragma unroll
@@ -843,7 +846,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
                        P.ngroups, P.coef, P.group_of};
 
     // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
-    __builtin_amdgcn_s_setprio(2);  // the store phase ahead of the computing waves
 #pragma unroll
     for (int rd = 0; rd < 2; rd++) {
         if ((lane >> 5) == rd) {
@@ -867,7 +869,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         wave_lds_sync();
     }
 
-    __builtin_amdgcn_s_setprio(0);
     // ---- rare path, part 2: the second certificate (one counter update per wave) ----
     if (rare) {
         uint32_t nset;
