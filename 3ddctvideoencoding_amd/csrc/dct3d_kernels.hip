@@ -400,6 +400,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     if (cube0 >= P.n_cubes) return;
     const uint64_t n_marks = E.n_values / 32;
     const uint64_t m0 = (uint64_t)cube0 * CS / 32;
+    __builtin_amdgcn_s_setprio(3);  // marks and window loads ahead of the computing waves
     const bool lv = m0 + lane < n_marks;
     const uint64_t my = lv ? E.mark[m0 + lane] : 0;
     const uint64_t first = __shfl(my, 0, 64);
@@ -428,6 +429,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
             if (i < nwin) win[i] = w0 + i < E.n_words ? __builtin_bswap32(t[b]) : 0u;
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     wave_lds_sync();
     int32_t v[32];
     parse_values<32>(E, win, nwin, w0, fits, my, v);
