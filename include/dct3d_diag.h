@@ -28,7 +28,7 @@ int dct3d_bandwidth_probe_dev(dct3d_ctx *ctx, const uint8_t *d_in, void *d_out, 
 
 /* Memory-only twin of dct3d_encode_stacks_dev (bench support; d_q receives NOT a DCT): the encode
  * kernel's row loads, LDS staging and 1 KiB non-temporal stores of the same cubes, without the
- * transform, quantisation, certification or fixup.  Its rate is the ceiling the encode's own traffic
+ * transform, quantisation or certification.  Its rate is the ceiling the encode's own traffic
  * reaches on this device. */
 int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                              int32_t *d_q);
