@@ -413,7 +413,9 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;
     uint2 raw[D];
+    __builtin_amdgcn_s_setprio(3);
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
+    __builtin_amdgcn_s_setprio(0);
     if (blockIdx.x == 0 && P.replay_clear) {
 #pragma unroll
         for (int i = 0; i < 2 * kCountSpread / kBlock; i++) P.replay_clear[i * kBlock + threadIdx.x] = 0u;

@@ -240,7 +240,9 @@ __global__ __launch_bounds__(kBlock, 4) void cube_f32_kernel(const float* __rest
     if (cube0 >= n_cubes) return;  // wave-uniform
     {
         int4 v[8];
+        __builtin_amdgcn_s_setprio(3);
         dec_load_tile_p<D>((const char*)in, n_cubes, cube0, lane, v);
+        __builtin_amdgcn_s_setprio(0);
         dec_stage_tile<D>(wl, lane, v);
     }
     wave_lds_sync();
