@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel(DecodeParams P) {
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * DecGeom<D>::CPW;
+    const uint32_t cube0 = (xcd_tile() * kWavesPerBlock + wave) * DecGeom<D>::CPW;
     int4 v[8];
     __builtin_amdgcn_s_setprio(3);  // a starting wave issues its loads ahead of the computing ones
     dec_load_tile<D>(P, cube0, lane, v);

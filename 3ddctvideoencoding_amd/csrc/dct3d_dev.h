@@ -24,6 +24,13 @@ static_assert(4 * 8 * kFace <= kWaveLds, "staging round must fit the wave region
 // per-wave LDS of the encode kernels: 8x8x4 moves its transpose and staging in two half rounds
 // (4.5 KiB), so that LDS does not cap it at 16 waves per CU (it needs 96 VGPRs: 5 waves per SIMD)
 template <int D> constexpr int enc_wave_lds() { return D == 8 ? kWaveLds : kWaveLds / 2; }
+
+// XCD-aware tile order: the dispatcher deals blocks to the 8 XCDs round-robin; block b takes tile
+// (b % 8) * (nb / 8) + b / 8, so each XCD (its own L2) walks a contiguous eighth of the data
+__device__ __forceinline__ uint32_t xcd_tile() {
+    const uint32_t nb8 = gridDim.x / 8u;
+    return blockIdx.x < nb8 * 8u ? (blockIdx.x & 7u) * nb8 + (blockIdx.x >> 3) : blockIdx.x;
+}
 static_assert(4 * 4 * kFace <= kWaveLds / 2, "8x8x4 staging round must fit the half region");
 
 // Wave-level ordering of LDS traffic between lanes of ONE wave: a compiler fence (LDS instructions

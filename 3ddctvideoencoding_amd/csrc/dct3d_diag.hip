@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_kernel_diag(DecodeParams P) 
     using G = DecGeom<D>;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * G::CPW;
+    const uint32_t cube0 = (xcd_tile() * kWavesPerBlock + wave) * G::CPW;  // the product's order
     int4 v[8];
     if (MODE == 2) {
         for (int t = 0; t < 8; t++) v[t] = make_int4(lane + t, (int)cube0 & 7, t, 1);

@@ -796,11 +796,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     __shared__ float4 s_tab[kTabN];
     __shared__ double s_b64[96];  // second certificate tables (rare path)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    // XCD-aware tile order: the dispatcher deals blocks to the 8 XCDs round-robin; block b takes tile
-    // (b % 8) * (nb / 8) + b / 8, so each XCD walks its own contiguous eighth of the raster
-    const uint32_t nb8 = gridDim.x / 8u;
-    const uint32_t bt = blockIdx.x < nb8 * 8u ? (blockIdx.x & 7u) * nb8 + (blockIdx.x >> 3) : blockIdx.x;
-    const uint32_t cube0 = P.g_base + (bt * kWavesPerBlock + wave) * kE16CPW;
+    const uint32_t cube0 = P.g_base + (xcd_tile() * kWavesPerBlock + wave) * kE16CPW;
     const int k = lane & 7, h = (lane >> 4) & 1;
     const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
     const uint32_t g = cube0 + c;

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(kBlock, 4) void cube_f32_kernel(const float* __rest
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = (blockIdx.x * kWavesPerBlock + wave) * CPW;
+    const uint32_t cube0 = (xcd_tile() * kWavesPerBlock + wave) * CPW;
     if (cube0 >= n_cubes) return;  // wave-uniform
     {
         int4 v[8];
