@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = P.cube_base + (blockIdx.x * kWavesPerBlock + wave) * CPW;
+    const uint32_t cube0 = P.cube_base + (xcd_tile() * kWavesPerBlock + wave) * CPW;
     if (cube0 >= P.n_cubes) return;
     const uint64_t n_marks = E.n_values / 32;
     const uint64_t m0 = (uint64_t)cube0 * CS / 32;
