@@ -25,11 +25,21 @@ static_assert(4 * 8 * kFace <= kWaveLds, "staging round must fit the wave region
 // (4.5 KiB), so that LDS does not cap it at 16 waves per CU (it needs 96 VGPRs: 5 waves per SIMD)
 template <int D> constexpr int enc_wave_lds() { return D == 8 ? kWaveLds : kWaveLds / 2; }
 
-// XCD-aware tile order: the dispatcher deals blocks to the 8 XCDs round-robin; block b takes tile
-// (b % 8) * (nb / 8) + b / 8, so each XCD (its own L2) walks a contiguous eighth of the data
+// XCD-aware tile order: the dispatcher deals blocks to the 8 XCDs round-robin, so consecutive tiles
+// land on 8 different XCDs (each with its own L2).  G = 0: block b takes tile (b % 8) * (nb / 8) + b / 8,
+// each XCD walks a contiguous eighth of the data; G > 0: each XCD walks runs of G consecutive tiles
+// (tiles 8G apart between its runs).  Measured per kernel (profiles/r02/variant_sweep.txt).
+template <uint32_t G = 0>
 __device__ __forceinline__ uint32_t xcd_tile() {
-    const uint32_t nb8 = gridDim.x / 8u;
-    return blockIdx.x < nb8 * 8u ? (blockIdx.x & 7u) * nb8 + (blockIdx.x >> 3) : blockIdx.x;
+    if constexpr (G == 0) {
+        const uint32_t nb8 = gridDim.x / 8u;
+        return blockIdx.x < nb8 * 8u ? (blockIdx.x & 7u) * nb8 + (blockIdx.x >> 3) : blockIdx.x;
+    } else {
+        const uint32_t full = gridDim.x / (8u * G) * (8u * G);
+        if (blockIdx.x >= full) return blockIdx.x;
+        const uint32_t r = blockIdx.x >> 3;
+        return (r / G) * (8u * G) + (blockIdx.x & 7u) * G + (r % G);
+    }
 }
 static_assert(4 * 4 * kFace <= kWaveLds / 2, "8x8x4 staging round must fit the half region");
 

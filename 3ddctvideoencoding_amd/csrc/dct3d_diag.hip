@@ -32,7 +32,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_memonly_kernel(EncodeParams 
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
     constexpr int NB = (D == 8) ? 8 : 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;  // the product's order
+    const uint32_t cube0 = P.g_base + (xcd_tile<64>() * kWavesPerBlock + wave) * kCubesPerWave;  // the product's order
     uint2 raw[D];
     load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);
     if (cube0 >= P.n_cubes) return;

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_kernel(EncodeParams P) {
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
     __shared__ float4 s_tab[kTabN];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = P.g_base + (blockIdx.x * kWavesPerBlock + wave) * kCubesPerWave;  // (XCD order: slower)
+    const uint32_t cube0 = P.g_base + (xcd_tile<64>() * kWavesPerBlock + wave) * kCubesPerWave;
     uint2 raw[D];
     __builtin_amdgcn_s_setprio(3);
     load_rows<D, NTL>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
@@ -796,7 +796,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     __shared__ float4 s_tab[kTabN];
     __shared__ double s_b64[96];  // second certificate tables (rare path)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = P.g_base + (xcd_tile() * kWavesPerBlock + wave) * kE16CPW;
+    const uint32_t cube0 = P.g_base + (xcd_tile<64>() * kWavesPerBlock + wave) * kE16CPW;
     const int k = lane & 7, h = (lane >> 4) & 1;
     const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
     const uint32_t g = cube0 + c;
