@@ -321,7 +321,7 @@ class Context:
                "dct3d_encode_diag_dev")
 
     def decode_diag_dev(self, d_q, width: int, height: int, n_stacks: int, d_frames, mode: int) -> None:
-        """Diagnostic: the 8x8x8 decode's memory part (mode 1) or compute part (mode 2) alone."""
+        """Diagnostic: the decode's memory part (mode 1) or compute part (mode 2) alone."""
         _check(diag_lib().dct3d_decode_diag_dev(self._h, _tptr(d_q), width, height, n_stacks, _tptr(d_frames), mode),
                "dct3d_decode_diag_dev")
 

@@ -383,7 +383,6 @@ int dct3d_decode_diag_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_
     int rc = view(c, v);
     uint64_t n_cubes = 0;
     if (rc || (rc = geometry(w, h, n_stacks, &n_cubes))) return rc;
-    if (v.bd != 8) return DCT3D_EINVAL;  // the split exists for the 8x8x8 decode
     if (n_cubes == 0) return DCT3D_OK;
     DecodeParams P;
     memset(&P, 0, sizeof(P));
@@ -396,13 +395,18 @@ int dct3d_decode_diag_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int n_
     P.div_nbx = fast_div(P.nbx);
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
-    P.stack_stride = P.plane * 8;
+    P.stack_stride = P.plane * v.bd;
     P.blk_store = mode == 1 && P.nbx % 2 == 0 && P.stack_stride < (1ull << 32) ? 1u : 0u;  // as the product (mode 2 stores nothing)
     P.inv_coef_t = nullptr;  // no replay: mode 1 certifies nothing, mode 2 stores (and so flags) nothing
-    const uint32_t per = DecGeom<8>::CPW * kWavesPerBlock;
+    const uint32_t per = (v.bd == 8 ? DecGeom<8>::CPW : DecGeom<4>::CPW) * kWavesPerBlock;
     const uint32_t groups = (uint32_t)((n_cubes + per - 1) / per);
-    if (mode == 1) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, v.stream, P);
-    else hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, v.stream, P);
+    if (v.bd == 8) {
+        if (mode == 1) hipLaunchKernelGGL((decode_kernel_diag<8, 1>), dim3(groups), dim3(kBlock), 0, v.stream, P);
+        else hipLaunchKernelGGL((decode_kernel_diag<8, 2>), dim3(groups), dim3(kBlock), 0, v.stream, P);
+    } else {
+        if (mode == 1) hipLaunchKernelGGL((decode_kernel_diag<4, 1>), dim3(groups), dim3(kBlock), 0, v.stream, P);
+        else hipLaunchKernelGGL((decode_kernel_diag<4, 2>), dim3(groups), dim3(kBlock), 0, v.stream, P);
+    }
     return hipGetLastError() == hipSuccess ? DCT3D_OK : DCT3D_EKERNEL;
 }
 

@@ -782,7 +782,8 @@ __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2
 // staging and stores with the transform, quantisation and certification replaced by a few integer ops.
 // MODE 2 (compute only, DIAGNOSTIC): ramp-like rows made from the lane and cube indices instead of the
 // loads, the whole transform / quantise / certify / staging, the stores suppressed by a runtime
-// condition (P.width == 0 never holds), so its time is the kernel's issue work alone.
+// condition (P.width == 0 never holds) and the rare paths skipped, so its time is the kernel's main-path
+// issue work alone.
 // One launch is the whole encode: no flag list, no counter reset, no fixup launch.  Block 0 zeroes the
 // next call's counter slot (P.replay_clear; the two slots alternate between calls).  7 waves per SIMD
 // (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (they
@@ -835,7 +836,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     }
     // ---- rare path, part 1: the second certificate's loads, issued before the stores (a load issued
     //      after them would wait for them too: one in-order vmcnt) ----
-    const bool rare = !MEM && P.recheck && __builtin_expect(__ballot(fm != 0u) != 0ull, 0);  // wave-uniform
+    const bool rare = !MEM && !COMP && P.recheck && __builtin_expect(__ballot(fm != 0u) != 0ull, 0);  // wave-uniform
     uint2 raw2[4];
     double bv = 0.0, tv = 0.0;
     if (rare) {
@@ -886,7 +887,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     //      the stored value by lane 0.  Its loads wait for the wave's stores (one in-order vmcnt), and
     //      lane 0's store follows its own earlier store of that word (vmcnt(0)), so the exact value is
     //      the one that stays. ----
-    if (__builtin_expect(!MEM && __ballot(fm != 0u) != 0ull, 0)) {
+    if (__builtin_expect(!MEM && !COMP && __ballot(fm != 0u) != 0ull, 0)) {
         char* rs = wl;  // the wave's region is free again (its last staging round is stored)
         uint32_t n = 0;
         for (;;) {

@@ -192,7 +192,7 @@ def measure_ceiling(ctx, torch, frames, q, reps, geom=None, dec_geom=None):
     mix = u8 read + int32 NT write (1:4, the encode's algorithmic bytes), copy, write-only, read-only.
     geom = (width, height, stacks, bytes_per_cube) for encode configs: also the encode kernel's own
     traffic without its compute (dct3d_encode_memonly_dev: same loads, LDS staging, NT stores).
-    dec_geom = (width, height, stacks, raster_out) for the 8x8x8 decode: its memory part and its compute
+    dec_geom = (width, height, stacks, raster_out) for the decode: its memory part and its compute
     part alone (dct3d_decode_diag_dev modes 1 / 2; libdct3d_diag.so)."""
     n_px = frames.numel() // 16 * 16
     out = {}
@@ -438,7 +438,7 @@ def main():
     ceiling = None if a.no_ceiling or q is None or not stacks else measure_ceiling(
         ctx, torch, frames, q, max(3, a.steps // 2),
         geom=(width, height, stacks, cs * 5) if direction == "encode" else None,
-        dec_geom=(width, height, stacks, torch.empty_like(frames)) if direction == "decode" and depth == 8 else None)
+        dec_geom=(width, height, stacks, torch.empty_like(frames)) if direction == "decode" else None)
 
     bytes_per_cube = cs * (1 + 4)  # u8 in + int32 out (encode) / int32 in + u8 out (decode)
     if direction in ("forward_f32", "inverse_f32"):

@@ -38,10 +38,10 @@ int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width,
 int dct3d_encode_diag_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                           int32_t *d_q, int mode);
 
-/* The 8x8x8 decode kernel split in two (bench support; d_raster receives NOT a decode): mode 1 = memory
- * only (the same staged loads and raster stores, no transform), mode 2 = compute only (no global loads,
- * no stores).  The decode's time read against both shows how far its memory and its fp64 issue overlap
- * (DESIGN.md §4).  8x8x8 contexts only. */
+/* The decode kernel split in two (bench support; d_raster receives NOT a decode): mode 1 = memory only
+ * (the same staged loads and raster stores, no transform), mode 2 = compute only (no global loads, no
+ * stores).  The decode's time read against both shows how far its memory and its fp64 issue overlap
+ * (DESIGN.md §4).  8x8x8 and 8x8x4 contexts. */
 int dct3d_decode_diag_dev(dct3d_ctx *ctx, const int32_t *d_q, int width, int height, int n_stacks,
                           uint8_t *d_raster, int mode);
 
