@@ -322,7 +322,7 @@ __device__ __forceinline__ void enc4_replay(const EncodeParams& P, const uint2 (
 #pragma unroll 1
             for (int gi = 0; gi < ng; gi++) acc = __dadd_rn(acc, prod[gi]);  // DCT.java:50, in order
             const int q = java_round_dev(__ddiv_rn(acc, (double)max(1, 5 * (kx + ky + kz))));
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after this lane's staged store of the word
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // after the wave's staged stores (one in-order count)
             P.out[(size_t)(cube0 + c) * CS + k] = q;
         }
         nrep += (uint32_t)__builtin_popcountll(__ballot(act && j == 0));
