@@ -76,6 +76,10 @@ struct dct3d_ctx {
     DevBuf d_enc_counts;
     int enc_slot = 0;
     int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
+    bool slot_used = false;    // a counting kernel of the current call was enqueued into enc_slot
+    bool batch = false;        // a host entry point's chunks: one slot for the whole call (close_slot after)
+    uint64_t batch_units = 0;
+    hipEvent_t ev_switch = nullptr;  // orders a dct3d_ctx_set_stream switch after the old stream's work
     // host-pointer entry point staging
     DevBuf h_in, h_out, h_aux;
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
@@ -253,13 +257,23 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
         if (c->pe_in[i]) (void)hipEventDestroy(c->pe_in[i]);
         if (c->pe_done[i]) (void)hipEventDestroy(c->pe_done[i]);
     }
+    if (c->ev_switch) (void)hipEventDestroy(c->ev_switch);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
 
 int dct3d_ctx_set_stream(dct3d_ctx* c, void* s) {
     if (!c) return DCT3D_EINVAL;
-    c->stream = s ? (hipStream_t)s : c->own_stream;
+    const hipStream_t ns = s ? (hipStream_t)s : c->own_stream;
+    if (ns != c->stream) {
+        // work enqueued on the new stream runs after the old stream's: a later launch would otherwise
+        // overlap an earlier one whose block 0 clears the counter slot the later one counts into
+        if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
+        if ((!c->ev_switch && hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess) ||
+            hipEventRecord(c->ev_switch, c->stream) != hipSuccess || hipStreamWaitEvent(ns, c->ev_switch, 0) != hipSuccess)
+            return DCT3D_EDEVICE;
+    }
+    c->stream = ns;
     return DCT3D_OK;
 }
 
@@ -366,14 +380,45 @@ static int check_geometry(const dct3d_ctx* c, int w, int h, int n_stacks, uint64
 
 // Decode: uncertified cubes are replayed inside the wave; the replay count goes to the ctx's current
 // counter slot, and the launch zeroes the other one for the next call (see d_enc_counts).
+static void set_count_slot(dct3d_ctx* c, unsigned int*& count, unsigned int*& clear) {
+    count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
+    clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+}
 static void set_dec_replay(dct3d_ctx* c, DecodeParams& P) {
     P.inv_coef_t = (const double*)c->d_inv_coef.p;
-    P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
-    P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+    set_count_slot(c, P.replay_count, P.replay_clear);
 }
-static void end_dec_replay(dct3d_ctx* c) {  // the slot counts replayed pixels (n_flagged)
+// A call's counting kernels are enqueued: its statistics are in enc_slot (units of work: `units`).  The
+// slot flips at the end of the call -- of every chunk together inside a host entry point's pipeline
+// (batch), and whenever a counting kernel was enqueued, even if a later step of the call failed (the
+// next call must start on the slot this one's launches zeroed).
+static void count_slot_used(dct3d_ctx* c, uint64_t units) {
+    c->slot_used = true;
+    if (c->batch) {
+        c->batch_units += units;
+        return;
+    }
     c->last_count_slot = c->enc_slot;
     c->enc_slot ^= 1;
+    c->slot_used = false;
+    c->last_units = units;
+    c->last_valid = true;
+}
+static void batch_begin(dct3d_ctx* c) {
+    c->batch = true;
+    c->batch_units = 0;
+    c->slot_used = false;
+    c->last_valid = false;
+    c->last_count_slot = -1;
+}
+static void batch_end(dct3d_ctx* c) {
+    c->batch = false;
+    if (!c->slot_used) return;
+    c->last_count_slot = c->enc_slot;
+    c->enc_slot ^= 1;
+    c->slot_used = false;
+    c->last_units = c->batch_units;
+    c->last_valid = true;
 }
 
 static int forward_f64_raster(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, uint64_t n_cubes, double* d_out) {
@@ -396,8 +441,10 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    c->last_valid = false;
-    c->last_count_slot = -1;
+    if (!c->batch) {
+        c->last_valid = false;
+        c->last_count_slot = -1;
+    }
     if (n_cubes == 0) return DCT3D_OK;
     const int D = c->bd;
     // one launch: uncertified coefficients are replayed inside the wave (exact Java fold)
@@ -422,8 +469,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     P.ngroups = (const int32_t*)c->d_ngroups.p;
     P.coef = (const double*)c->d_coef.p;
     P.group_of = (const uint8_t*)c->d_group_of.p;
-    P.replay_count = (unsigned int*)c->d_enc_counts.p + c->enc_slot * 2 * kCountSpread;
-    P.replay_clear = (unsigned int*)c->d_enc_counts.p + (c->enc_slot ^ 1) * 2 * kCountSpread;
+    set_count_slot(c, P.replay_count, P.replay_clear);
     P.tab64 = (const double*)c->d_tabs64.p;
     P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
     hipEvent_t* ev = timing_slot(c);
@@ -434,10 +480,7 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
         (void)hipEventRecord(ev[2], c->stream);
         (void)hipEventRecord(ev[3], c->stream);
     }
-    c->last_count_slot = c->enc_slot;
-    c->enc_slot ^= 1;
-    c->last_units = n_cubes * (uint64_t)c->plan.cs;
-    c->last_valid = true;
+    count_slot_used(c, n_cubes * (uint64_t)c->plan.cs);
     if (d_dct) return forward_f64_raster(c, d_raster, w, h, n_cubes, d_dct);
     return DCT3D_OK;
 }
@@ -448,8 +491,10 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
     int rc = check_geometry(c, w, h, n_stacks, &n_cubes);
     if (rc) return rc;
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-    c->last_valid = false;
-    c->last_count_slot = -1;
+    if (!c->batch) {
+        c->last_valid = false;
+        c->last_count_slot = -1;
+    }
     if (n_cubes == 0) return DCT3D_OK;
     const int D = c->bd;
     const uint64_t plane = (uint64_t)w * h;
@@ -480,9 +525,7 @@ int dct3d_decode_stacks_dev(dct3d_ctx* c, const int32_t* d_q, int w, int h, int 
         (void)hipEventRecord(ev[2], c->stream);
         (void)hipEventRecord(ev[3], c->stream);
     }
-    end_dec_replay(c);
-    c->last_units = n_cubes * (uint64_t)c->plan.cs;
-    c->last_valid = true;
+    count_slot_used(c, n_cubes * (uint64_t)c->plan.cs);
     return DCT3D_OK;
 }
 
@@ -604,10 +647,13 @@ int dct3d_encode_stacks(dct3d_ctx* c, const uint8_t* raster, int w, int h, int n
     const size_t in_bytes = n_cubes * c->plan.cs, out_bytes = in_bytes * sizeof(int32_t);
     if (!dct) {  // pipelined
         const size_t px = in_bytes / n_stacks;
-        return run_pipeline(c, n_stacks, px, px * sizeof(int32_t), raster, q,
-                            [&](const void* din, void* dout, int, int ns) {
-                                return dct3d_encode_stacks_dev(c, (const uint8_t*)din, w, h, ns, (int32_t*)dout, nullptr);
-                            });
+        batch_begin(c);  // every chunk counts into one slot: dct3d_get_stats reports the whole call
+        rc = run_pipeline(c, n_stacks, px, px * sizeof(int32_t), raster, q,
+                          [&](const void* din, void* dout, int, int ns) {
+                              return dct3d_encode_stacks_dev(c, (const uint8_t*)din, w, h, ns, (int32_t*)dout, nullptr);
+                          });
+        batch_end(c);
+        return rc;
     }
     if ((rc = c->h_in.grow(in_bytes)) || (rc = c->h_out.grow(out_bytes))) return rc;
     if (hipMemcpyAsync(c->h_in.p, raster, in_bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
@@ -629,9 +675,12 @@ int dct3d_decode_stacks(dct3d_ctx* c, const int32_t* q, int w, int h, int n_stac
     if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
     if (n_cubes == 0) return DCT3D_OK;
     const size_t px = n_cubes * c->plan.cs / n_stacks;
-    return run_pipeline(c, n_stacks, px * sizeof(int32_t), px, q, raster, [&](const void* din, void* dout, int, int ns) {
+    batch_begin(c);
+    rc = run_pipeline(c, n_stacks, px * sizeof(int32_t), px, q, raster, [&](const void* din, void* dout, int, int ns) {
         return dct3d_decode_stacks_dev(c, (const int32_t*)din, w, h, ns, (uint8_t*)dout);
     });
+    batch_end(c);
+    return rc;
 }
 
 // ---- drop-in (A): float cube-major <-> float cube-major --------------------------------------
@@ -1007,6 +1056,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
         (void)hipEventRecord(ev[2], c->stream);
         (void)hipEventRecord(ev[3], c->stream);
     }
+    count_slot_used(c, (uint64_t)ns * cps * (uint64_t)c->plan.cs);
     return DCT3D_OK;
 }
 extern "C" {
@@ -1028,9 +1078,6 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     EgDecParams E;
     if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
     if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
-    end_dec_replay(c);
-    c->last_units = n_cubes * (uint64_t)c->plan.cs;
-    c->last_valid = true;
     return eg_decode_status(c, E, end_bit);
 }
 
@@ -1050,13 +1097,12 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E))) return rc;
     // the raster leaves in chunks of stacks while the next chunk decodes (the stream is small: no upload)
     const size_t px = n_cubes * c->plan.cs / n_stacks;
+    batch_begin(c);
     rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
         return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
     });
+    batch_end(c);
     if (rc) return rc;
-    end_dec_replay(c);
-    c->last_units = n_cubes * (uint64_t)c->plan.cs;
-    c->last_valid = true;
     return eg_decode_status(c, E, end_bit);
 }
 

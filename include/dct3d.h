@@ -195,9 +195,7 @@ int dct3d_encode_eg(dct3d_ctx *ctx, const uint8_t *raster, int width, int height
  * transform kernel, and each wave codes its 8 cubes straight into the stream.  The stream format,
  * carry, d_out and *total_bits are those of dct3d_eg_encode_dev (the bytes are identical to
  * dct3d_encode_stacks_dev followed by dct3d_eg_encode_dev).  DCT3D_ENOSPC when out_cap is too small
- * (*total_bits is still set; d_out is untouched -- with DCT3D_EG_SINGLE_PASS=1 in the environment,
- * nothing is written past out_cap, but segments that fit may have been: each wave places its bits as
- * soon as its offset is known, before the total is).  Synchronises the context stream. */
+ * (*total_bits is still set; d_out is untouched).  Synchronises the context stream. */
 int dct3d_encode_eg_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                         uint8_t carry_byte, int carry_bits, uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
 

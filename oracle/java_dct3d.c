@@ -28,7 +28,11 @@
  *       sums per 8^3 cube; 4,301 per 8x8x4),
  *   (3) an independent arbitrary-precision evaluation of the DCT formula (quantised ints must
  *       agree wherever the exact value is not within 1e-9 of a rounding tie).
- * Residual unpinned item: Java's Math.cos is only specified to 1 ulp; glibc cos() is used.
+ * Residual unpinned item: Math.cos differs from the correctly rounded value.  glibc cos() is used
+ * and is correctly rounded at every argument the plan evaluates; every group key except those of
+ * the exactly rational coefficients (+-1/32, +-1/16) is stable under any 1-ulp cosine error
+ * (tests/test_plan.py::test_libm_cos_correctly_rounded_at_plan_arguments,
+ * ::test_grouping_keys_stable_under_cos_ulp).
  *
  * Build: see oracle/Makefile (gcc -O2 -ffp-contract=off; no FMA contraction, like javac/HotSpot).
  */

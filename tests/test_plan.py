@@ -153,3 +153,93 @@ def test_hashmap_fold_order_closed_form(pkg, plan8, plan4, depth):
         assert np.array_equal(p["coef"][k, :ng], coefs), k          # bit-identical, same order
         assert np.array_equal(np.where(p["group_of"][k] == 0xFF, -1, p["group_of"][k].astype(np.int64)), gof), k
         assert np.array_equal(np.array([c for c, _ in oplan.groups(k)]), coefs), k
+
+
+def _cos_args(n):
+    """Every argument DCT.initialize / InverseDCT.initialize pass to Math.cos for one axis of length n
+    (DCT.java:104-112, InverseDCT.java:110-124): (Math.PI / (float) n) * (m + 0.5f) * k, left to right."""
+    import math
+    f32 = lambda v: float(np.float32(v))
+    p = math.pi / f32(n)
+    return {(m, k): p * f32(m + 0.5) * k for m in range(n) for k in range(n)}
+
+
+def test_libm_cos_correctly_rounded_at_plan_arguments():
+    """VERDICT r2 #6 (Math.cos residual): Java's Math.cos is specified only to 1 ulp, the planner, the
+    oracle and this interpreter use glibc cos.  At every argument the Java plan evaluates (8-point and
+    4-point axes), glibc returns the correctly rounded cosine (mpmath at 60 digits), so the planner's
+    coefficient bits equal those of any Java whose Math.cos is correctly rounded there."""
+    import math
+    import mpmath
+    mpmath.mp.dps = 60
+    for n in (8, 4):
+        for (m, k), a in _cos_args(n).items():
+            exact = mpmath.cos(mpmath.mpf(a))          # the double a, exactly, then cos to 60 digits
+            got = math.cos(a)
+            # correctly rounded: |exact - cos(a)| <= half an ulp of cos(a)
+            assert abs(exact - mpmath.mpf(got)) <= mpmath.mpf(math.ulp(got)) / 2, (n, m, k, a)
+
+
+def _plan_coefficients(depth):
+    """Every DCT.initialize coefficient (DCT.java:104-112) as [k0, k1, k2, n0, n1, n2] float64, the
+    product evaluated left to right as javac does, with glibc cos, plus the number of non-trivial
+    cosine factors (k != 0: cos(0) = 1 exactly in any libm) of each."""
+    import math
+    cd = depth
+    scale = math.sqrt(math.pow(2.0, 3.0)) / math.sqrt(64 * cd)
+    inv_sqrt2 = 1.0 / math.sqrt(2.0)
+    ax = {n: _cos_args(n) for n in (8, 4)}
+    cosd = np.array([[math.cos(ax[cd][(m, k)]) for m in range(cd)] for k in range(cd)])   # [k][n]
+    cosh = np.array([[math.cos(ax[8][(m, k)]) for m in range(8)] for k in range(8)])
+    cvec = lambda n: np.array([inv_sqrt2] + [1.0] * (n - 1))
+    c = scale * cvec(cd)[:, None, None, None, None, None]
+    c = c * cvec(8)[None, :, None, None, None, None]
+    c = c * cvec(8)[None, None, :, None, None, None]
+    c = c * cosd[:, None, None, :, None, None]
+    c = c * cosh[None, :, None, None, :, None]
+    c = c * cosh[None, None, :, None, None, :]
+    nt = ((np.arange(cd) != 0)[:, None, None] + (np.arange(8) != 0)[None, :, None]
+          + (np.arange(8) != 0)[None, None, :]).astype(int)
+    return c, np.broadcast_to(nt[:, :, :, None, None, None], c.shape)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+def test_grouping_keys_stable_under_cos_ulp(depth):
+    """how far the Java grouping depends on Math.cos's last bit.  A cosine 1 ulp off the
+    correctly rounded one moves a coefficient by at most ~3 ulp (plus re-roundings of the product); the
+    group key is (long)(c * 1E9) (DCT.java:115).
+      * Every coefficient whose exact real value times 1E9 is NOT an integer keeps its key under any
+        relative move of 2^-44 (~200x the largest 1-ulp effect).
+      * The others are the rational coefficients: c = +-1/32 or +-1/16 exactly (e.g. k = (0, 2, 2) at
+        8^3: 1/8 * 1/sqrt2 * cos(pi/8) cos(3pi/8) = 1/32; 8x8x4's k0 = 2 row is +-sqrt2/2).  Their fp64
+        values straddle the integer key (31249999.99999999 -> 31249999, 31250000.0 -> 31250000), so their
+        keys -- hence the groups and the HashMap fold order of those k -- are decided by the cosine bits.
+        For them the plan equals Java's iff Math.cos is correctly rounded at their arguments, which is what
+        glibc returns (test_libm_cos_correctly_rounded_at_plan_arguments).  The residual is therefore
+        exactly: "a JVM whose Math.cos is not correctly rounded at one of these arguments"."""
+    import mpmath
+    mpmath.mp.dps = 40
+    c, nt = _plan_coefficients(depth)
+    x = c * 1e9
+    eps = 2.0 ** -44
+    moved = (np.trunc(x * (1 - eps)) != np.trunc(x * (1 + eps))) & (nt > 0)
+    # every key that can move belongs to a coefficient whose exact value * 1E9 is an integer
+    kk = np.argwhere(moved)
+    exact_rational = {}
+    for k0, k1, k2, n0, n1, n2 in kk:
+        key = (int(k0), int(k1), int(k2), int(n0), int(n1), int(n2))
+        cd = depth
+        e = (mpmath.sqrt(8) / mpmath.sqrt(64 * cd)
+             * (1 / mpmath.sqrt(2) if k0 == 0 else 1) * (1 / mpmath.sqrt(2) if k1 == 0 else 1)
+             * (1 / mpmath.sqrt(2) if k2 == 0 else 1)
+             * mpmath.cos(mpmath.pi / cd * (n0 + mpmath.mpf(1) / 2) * k0)
+             * mpmath.cos(mpmath.pi / 8 * (n1 + mpmath.mpf(1) / 2) * k1)
+             * mpmath.cos(mpmath.pi / 8 * (n2 + mpmath.mpf(1) / 2) * k2)) * 10 ** 9
+        assert abs(e - mpmath.nint(e)) < mpmath.mpf(10) ** -20, key
+        exact_rational[key[:3]] = exact_rational.get(key[:3], 0) + 1
+    # the sensitive outputs: 24 at 8^3 (kz, ky, kx in {0, 2, 6} patterns), 39 at 8x8x4
+    assert len(exact_rational) == {8: 24, 4: 39}[depth], len(exact_rational)
+    # all other keys sit far from an integer boundary
+    nz = (np.abs(x) >= 1.0) & ~moved & (nt > 0)
+    frac = np.abs(x[nz] - np.round(x[nz])) / np.abs(x[nz])
+    assert frac.min() > eps, frac.min()
