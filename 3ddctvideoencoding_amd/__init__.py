@@ -30,6 +30,7 @@ INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
 # test / diagnostic options (include/dct3d.h, Context.set_option)
 DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 2, 3, 5, 6
+DCT3D_OPT_ENC_STAGGER = 7
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -44,7 +45,7 @@ ABI_SYMBOLS = (
 )
 # Every symbol include/dct3d_diag.h declares (libdct3d_diag.so; none of them is in libdct3d.so).
 DIAG_SYMBOLS = ("dct3d_fill_synthetic_dev", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
-                "dct3d_encode_diag_dev", "dct3d_decode_diag_dev")
+                "dct3d_encode_diag_dev", "dct3d_encode_trace_dev", "dct3d_decode_diag_dev")
 
 
 class Dct3dError(RuntimeError):
@@ -135,6 +136,7 @@ def diag_lib() -> C.CDLL:
         D.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
         D.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
         D.dct3d_encode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
+        D.dct3d_encode_trace_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32, vp]
         D.dct3d_decode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
         _diag = D
     return _diag
@@ -319,6 +321,12 @@ class Context:
         """Diagnostic: the encode's memory part (mode 1) or, 8x8x8, its compute part (mode 2) alone."""
         _check(diag_lib().dct3d_encode_diag_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q), mode),
                "dct3d_encode_diag_dev")
+
+    def encode_trace_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q, d_trace) -> None:
+        """Diagnostic: the product encode (8x8x8) with a per-wave timeline in d_trace (uint64, 4 per wave:
+        start, transform done, stores issued -- 100 MHz clock -- and XCC_ID << 32 | HW_ID)."""
+        _check(diag_lib().dct3d_encode_trace_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q), 3,
+                                                 _tptr(d_trace)), "dct3d_encode_trace_dev")
 
     def decode_diag_dev(self, d_q, width: int, height: int, n_stacks: int, d_frames, mode: int) -> None:
         """Diagnostic: the decode's memory part (mode 1) or compute part (mode 2) alone."""

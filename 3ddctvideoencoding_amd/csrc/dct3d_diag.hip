@@ -331,12 +331,18 @@ int dct3d_encode_memonly_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h
 }
 
 int dct3d_encode_diag_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode) {
+    return dct3d_encode_trace_dev(c, d_raster, w, h, n_stacks, d_q, mode, nullptr);
+}
+
+int dct3d_encode_trace_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode,
+                           uint64_t* d_trace) {
     CtxView v;
     if ((!d_raster || !d_q) && n_stacks) return DCT3D_EINVAL;
     int rc = view(c, v);
     uint64_t n_cubes = 0;
     if (rc || (rc = geometry(w, h, n_stacks, &n_cubes))) return rc;
-    if (mode != 1 && !(mode == 2 && v.bd == 8)) return DCT3D_EINVAL;
+    if (mode != 1 && !((mode == 2 || mode == 3) && v.bd == 8)) return DCT3D_EINVAL;
+    if (mode == 3 && !d_trace) return DCT3D_EINVAL;
     if (n_cubes == 0) return DCT3D_OK;
     EncodeParams P;
     memset(&P, 0, sizeof(P));
@@ -367,7 +373,9 @@ int dct3d_encode_diag_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, i
             P.ngroups = t->ngroups;
             P.coef = t->coef;
             P.group_of = t->group_of;
-            hipLaunchKernelGGL((encode16_kernel<true, 2>), grid, dim3(kBlock), 0, v.stream, P);
+            P.trace = d_trace;
+            if (mode == 2) hipLaunchKernelGGL((encode16_kernel<true, 2>), grid, dim3(kBlock), 0, v.stream, P);
+            else hipLaunchKernelGGL((encode16_kernel<true, 3>), grid, dim3(kBlock), 0, v.stream, P);
         }
     } else {
         const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;

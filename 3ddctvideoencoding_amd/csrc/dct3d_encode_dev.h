@@ -792,7 +792,9 @@ static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the
 template <bool NT, int MODE = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
-    constexpr bool MEM = MODE == 1, COMP = MODE == 2;
+    constexpr bool MEM = MODE == 1, COMP = MODE == 2, TRACE = MODE == 3;
+    uint64_t t_start = 0, t_comp = 0;
+    if constexpr (TRACE) t_start = __builtin_amdgcn_s_memrealtime();
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
     __shared__ float4 s_tab[kTabN];
     __shared__ double s_b64[96];  // second certificate tables (rare path)
@@ -813,6 +815,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         // a starting wave computes its addresses and issues its loads at the top priority: under the
         // default oldest-first issue they queue behind the computing waves' VALU work, and a box whose
         // encode loses the overlap of memory and compute that way runs 10 % slower (variant_sweep.txt)
+        if constexpr (!MEM && !COMP) {
+            if (P.stagger && blockIdx.x < P.stagger_cus * P.stagger_layers) {
+                for (uint32_t i = (blockIdx.x / P.stagger_cus) * P.stagger; i; i--) __builtin_amdgcn_s_sleep(8);
+            }
+        }
         if constexpr (!MEM) __builtin_amdgcn_s_setprio(3);
         e16_load(P, g, valid, k, h, raw);
         if constexpr (!MEM) __builtin_amdgcn_s_setprio(0);
@@ -834,6 +841,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         enc_tables(P, s_tab, lane);
         e16_body(P, raw, wl, s_tab, lane, valid, qv, fm);
     }
+    if constexpr (TRACE) t_comp = __builtin_amdgcn_s_memrealtime();
     // ---- rare path, part 1: the second certificate's loads, issued before the stores (a load issued
     //      after them would wait for them too: one in-order vmcnt) ----
     const bool rare = !MEM && !COMP && P.recheck && __builtin_expect(__ballot(fm != 0u) != 0ull, 0);  // wave-uniform
@@ -872,6 +880,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         wave_lds_sync();
     }
 
+    if constexpr (TRACE) {  // the wave's timeline: start, transform done, stores issued (+ 100 MHz clock)
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | (0 << 6) | 20); // XCC_ID
+        if (lane == 0) {
+            uint64_t* tr = P.trace + (size_t)((cube0 - P.g_base) / kE16CPW) * 4;
+            *(ulonglong2*)tr = make_ulonglong2(t_start, t_comp);
+            *(ulonglong2*)(tr + 2) = make_ulonglong2(t_end, ((uint64_t)xcc << 32) | hw);
+        }
+    }
     // ---- rare path, part 2: the second certificate (one counter update per wave) ----
     if (rare) {
         uint32_t nset;

@@ -92,6 +92,17 @@ def parse():
                     help="N>1, encode configs: also time the optional host-of-record distribution (SURVEY.md §8e): "
                          "rank 0 scatters every rank's u8 stacks and gathers the int32 cubes back over RCCL p2p "
                          "(reported under 'xgmi', never part of 'value')")
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed steps for at least this much wall time before the warmup steps (the GPU's "
+                         "power-management transient, ~30 ms of load); 0 = off")
+    ap.add_argument("--kernel-events", default="separate", choices=["separate", "timed"],
+                    help="where the library's per-launch events (kernel_ms) run: a separate pass after the timed "
+                         "region (default) or inside it (adds their device cost to every step)")
+    ap.add_argument("--pad-mb", type=int, default=0,
+                    help="A/B: allocate this many MiB between the input and the output buffer (placement study)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B knob: a context option (DCT3D_OPT_<NAME>, dct3d_ctx_set_option) set before the run; "
+                         "options change how results are reached, never the results")
     ap.add_argument("--eg-two-step", action="store_true",
                     help="c7 / c8: the int32 cube-major intermediate plus the stand-alone Exp-Golomb stage (A/B)")
     return ap.parse_args()
@@ -185,6 +196,19 @@ def pmc_traffic(config: str, kernel: str, depth: int):
     if "FETCH_SIZE" not in vals or "WRITE_SIZE" not in vals:
         return None, None
     return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, os.path.relpath(path, REPO)
+
+
+def job_roofline(per_rank, bytes_per_cube, peak_per_gpu=HBM_PEAK_GBS):
+    """The job's roofline for N > 1: every rank's algorithmic bytes of one step, summed, over
+    the slowest rank's device time per step, against N x the per-GPU peak -- and the weakest rank's own
+    fraction beside it.  per_rank: [{"cubes", "device_ms_per_step", "frac"}, ...] (one entry per rank)."""
+    n = len(per_rank)
+    job_bytes = sum(r["cubes"] for r in per_rank) * bytes_per_cube
+    t_ms = max(r["device_ms_per_step"] for r in per_rank)
+    achieved = job_bytes / (t_ms * 1e-3) / 1e9 if t_ms > 0 else 0.0
+    return {"achieved": achieved, "peak": n * peak_per_gpu, "frac": achieved / (n * peak_per_gpu),
+            "job_bytes_per_step": job_bytes, "max_rank_device_ms_per_step": t_ms,
+            "min_rank_frac": min(r["frac"] for r in per_rank)}
 
 
 def measure_ceiling(ctx, torch, frames, q, reps, geom=None, dec_geom=None):
@@ -320,6 +344,9 @@ def main():
 
     pkg = importlib.import_module("3ddctvideoencoding_amd")
     ctx = pkg.Context(dev, 8, 8, depth)
+    for o in a.opt:
+        name, val = o.split("=", 1)
+        ctx.set_option(getattr(pkg, "DCT3D_OPT_" + name.upper()), float(val))
     # a dedicated stream: the library, torch's events and torch's allocations all use it (torch's
     # default stream has handle 0, which the C-ABI reads as "use the context's own stream")
     stream = torch.cuda.Stream()
@@ -331,6 +358,7 @@ def main():
     frames = torch.empty((max(1, stacks) * depth, height, width), dtype=torch.uint8, device="cuda")
     # each rank encodes different content (its own slice of one long synthetic video)
     ctx.fill_synthetic_dev(frames, width, height, stacks * depth, frame0=first * depth, kind=a.kind)
+    pad = torch.empty((a.pad_mb << 20,), dtype=torch.uint8, device="cuda") if a.pad_mb else None  # A/B: placement
     q = torch.empty((max(1, n_cubes) * cs,), dtype=torch.int32, device="cuda")
     eg_info = {}
     if direction == "decode":
@@ -404,10 +432,25 @@ def main():
             ctx.encode_stacks_dev(frames, width, height, stacks, q)
     torch.cuda.synchronize()
 
+    # settle: the GPU's power management needs ~30 ms of sustained load to reach its steady state -- a
+    # rocprofv3 trace of back-to-back launches shows kernel durations rising ~15 % over the first ~10
+    # launches and decaying back over the next ~50 (profiles/r03/power_transient/); untimed steps for
+    # at least --settle-ms of wall time come before the W warmup steps, so the K timed steps measure
+    # the steady state whatever W is
+    settle_steps, t_settle = 0, time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < a.settle_ms:
+        for _ in range(4):
+            step()
+        settle_steps += 4
+        torch.cuda.synchronize()
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    ctx.set_profiling(True)
+    # the library's per-launch events (kernel_ms) cost ~17 us of device time per step (event packets
+    # between the launches); by default they run in a separate pass after the timed region, so the timed
+    # steps are back-to-back launches only
+    events_timed = a.kernel_events == "timed"
+    ctx.set_profiling(events_timed)
     ctx.reset_timers()
     if dist:
         dist.barrier()
@@ -425,6 +468,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     dev_step_ms = ev_a.elapsed_time(ev_b) / a.steps
+    if not events_timed:  # the kernel-timing pass: the same steps again, each launch between events
+        ctx.set_profiling(True)
+        ctx.reset_timers()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
     st = ctx.stats()
     ctx.set_profiling(False)
     round_trip = None
@@ -491,11 +540,16 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "settle_steps": settle_steps,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64" if direction in ("decode", "decode_eg", "forward_f32", "inverse_f32") else "f32",
+        "dtype_note": ("fp64 arithmetic throughout" if direction in ("decode", "decode_eg", "forward_f32", "inverse_f32")
+                       else "fp32 butterflies certified per coefficient against the fp64 Java value; uncertified "
+                            "ones are settled by an fp64 recheck or the exact Java fold, so every output equals "
+                            "the fp64 Java result (not a reduced-precision result)"),
         "data": "synthetic",
         "config": {
             "workload": f"{width}x{height} grayscale, {depth}-frame stacks, "
@@ -508,6 +562,7 @@ def main():
             "job_stacks": job_stacks,
             "cubes_per_gpu_step": n_cubes,
             "content": a.kind,
+            "options": a.opt or None,
             "parallelism": f"dp{world} (stacks sharded, no data-path collective)",
         },
         "roofline": {
@@ -544,6 +599,16 @@ def main():
     }
     if per_rank is not None:
         res["per_rank"] = per_rank
+        # N > 1: roofline = the job aggregate (all ranks' bytes / the slowest rank's device time / N peaks);
+        # rank 0's own numbers stay under roofline.rank0_*
+        rf = res["roofline"]
+        rf["rank0_achieved"], rf["rank0_frac"] = rf["achieved"], rf["frac"]
+        agg = job_roofline(per_rank, bytes_per_cube)
+        rf.update(achieved=agg["achieved"], peak=agg["peak"], frac=agg["frac"],
+                  min_rank_frac=agg["min_rank_frac"], job_bytes_per_step=agg["job_bytes_per_step"],
+                  max_rank_device_ms_per_step=agg["max_rank_device_ms_per_step"],
+                  basis="job aggregate: the algorithmic bytes of every rank's step / the slowest rank's device "
+                        "time per step / (N x 8 TB/s); rank0_* and per_rank hold the per-rank rates")
     if xgmi is not None:
         res["xgmi"] = xgmi
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -37,6 +37,11 @@ int dct3d_encode_memonly_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width,
  * indices instead of the loads, the whole transform / quantise / certify / staging, no stores). */
 int dct3d_encode_diag_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                           int32_t *d_q, int mode);
+/* As dct3d_encode_diag_dev; mode 3 (8x8x8) = the product encode (d_q IS the encode) with a timeline:
+ * d_trace[4 w .. 4 w + 3] of wave w = {start, transform done, stores issued} on the 100 MHz
+ * s_memrealtime clock and (XCC_ID << 32 | HW_ID).  d_trace: 32 bytes per 4 cubes. */
+int dct3d_encode_trace_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
+                           int32_t *d_q, int mode, uint64_t *d_trace);
 
 /* The decode kernel split in two (bench support; d_raster receives NOT a decode): mode 1 = memory only
  * (the same staged loads and raster stores, no transform), mode 2 = compute only (no global loads, no

@@ -132,3 +132,41 @@ def test_bench_job_split():
         assert all(p == (r * 128, 128, None, "weak") for r, p in enumerate(w))
     assert bench.rank_stacks("c4_encode_4k", 8, None, 2, 1) == (8, 8, None, "weak")      # --stacks: weak
     assert bench.rank_stacks("c2_encode_1080p", None, 10, 4, 3) == (8, 2, 10, "strong")  # --job-stacks
+
+
+def _roofline_worker(rank, world, port, out_dir):
+    """Each rank's per-step record as bench.py gathers it (all_gather over the process group), then the
+    job aggregate bench.py reports for N > 1."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module("bench")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    cubes = [1036800, 1036800, 518400][rank]           # ragged shards, as a 2.5-stack split would be
+    ms = [0.50, 0.55, 0.30][rank]
+    frac = cubes * 2560 / (ms * 1e-3) / 1e9 / 8000.0
+    mine = torch.tensor([float(rank), 8.0, float(cubes), ms, frac], dtype=torch.float64)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    per_rank = [{"rank": int(r[0]), "stacks": int(r[1]), "cubes": int(r[2]), "device_ms_per_step": float(r[3]),
+                 "frac": float(r[4])} for r in (x.tolist() for x in allr)]
+    agg = bench.job_roofline(per_rank, 2560)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "agg.npy"), np.array([agg["achieved"], agg["peak"], agg["frac"],
+                                                            agg["min_rank_frac"]]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_job_roofline_gloo(tmp_path):
+    """for N > 1 bench.py reports roofline.frac as the job aggregate -- total
+    algorithmic bytes / max-over-ranks device time / (N x 8 TB/s) -- with the weakest rank's own frac
+    beside it (min_rank_frac), not rank 0's."""
+    mp.spawn(_roofline_worker, args=(3, _port(), str(tmp_path)), nprocs=3, join=True)
+    achieved, peak, frac, min_rank = np.load(tmp_path / "agg.npy")
+    job = (1036800 * 2 + 518400) * 2560
+    assert abs(achieved - job / 0.55e-3 / 1e9) < 1e-6 * achieved
+    assert peak == 3 * 8000.0
+    assert abs(frac - achieved / 24000.0) < 1e-12
+    assert abs(min_rank - 518400 * 2560 / 0.30e-3 / 1e9 / 8000.0) < 1e-12    # the half shard's own rate
+    assert frac < min_rank  # the ragged third rank idles while the slowest one finishes
