@@ -62,7 +62,15 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
     size_t eg_cap = stack_px * batch / 2 + 64;
     unsigned char *eg = host_eg ? NULL : (unsigned char *)malloc(eg_cap);
     dct3d_entropy_enc *ent = dct3d_entropy_enc_create(width, height, depth, out);
+    /* DCT3D_CODEC_DEFLATE_THREADS=N (N > 1): parallel deflate -- the same inflated payload, a different
+     * .bin; default: one zlib stream, the reference encoder's bytes */
+    const char *dt = getenv("DCT3D_CODEC_DEFLATE_THREADS");
+    const int deflate_threads = dt ? atoi(dt) : 1;
     int status = 0;
+    if (ent && dct3d_entropy_enc_set_threads(ent, deflate_threads, 0)) {
+        dct3d_entropy_enc_destroy(ent);
+        ent = NULL;
+    }
     if (!raster || (host_eg ? !q : !eg) || !ent) {
         printf("Out of memory\n");
         status = 1;

@@ -19,6 +19,12 @@ typedef struct dct3d_entropy_dec dct3d_entropy_dec;
 
 /* sink: FILE* (out) or, if out == NULL, an internal growable memory buffer */
 dct3d_entropy_enc *dct3d_entropy_enc_create(int width, int height, int depth, FILE *out);
+/* Optional, before the first push: deflate with `threads` worker threads (threads <= 1: the single zlib
+ * stream, byte-identical to the reference encoder's .bin -- the default).  The parallel form cuts the
+ * input into chunks of chunk_bytes (0: 256 KiB), deflates each at level 9 primed with the preceding
+ * 32 KiB, joins them with sync flushes inside one zlib stream: a different .bin whose inflated payload
+ * is the reference's. */
+int dct3d_entropy_enc_set_threads(dct3d_entropy_enc *e, int threads, size_t chunk_bytes);
 /* q: one stack of cubes, cube-major int32; is_last selects Z_FINISH (encoder.c:266-271) */
 int dct3d_entropy_enc_push(dct3d_entropy_enc *e, const int32_t *q, int is_last);
 /* the stream's current partial byte and the bits used in it (0..7): the carry for a stream built
@@ -50,6 +56,8 @@ int dct3d_codec_entropy_encode(const int32_t *q, int width, int height, int n_st
                                unsigned char **out, size_t *out_len);
 int dct3d_codec_entropy_decode(const unsigned char *bin, size_t len, int width, int height, int n_stacks, int depth,
                                int32_t *q);
+int dct3d_codec_entropy_encode_mt(const int32_t *q, int width, int height, int n_stacks, int depth, int threads,
+                                  size_t chunk_bytes, unsigned char **out, size_t *out_len);
 void dct3d_codec_free(void *p);
 
 #ifdef __cplusplus

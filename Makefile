@@ -46,10 +46,10 @@ $(DIAGLIB): $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(DIAG_SRCS)) $(LIB)
 
 $(CODECLIB): $(CODEC_LIB_SRCS) $(LIB) $(wildcard include/*.h)
 	@mkdir -p $(LIBDIR)
-	$(CC) $(CFLAGS) -shared -o $@ $(CODEC_LIB_SRCS) -L$(LIBDIR) -ldct3d -Wl,-rpath,'$$ORIGIN' -lz -lm
+	$(CC) $(CFLAGS) -shared -o $@ $(CODEC_LIB_SRCS) -L$(LIBDIR) -ldct3d -Wl,-rpath,'$$ORIGIN' -lz -lm -lpthread
 
 $(CLI): $(CSRC)/host/main.c $(CODECLIB)
-	$(CC) $(CFLAGS) -o $@ $< -L$(LIBDIR) -ldct3dcodec -ldct3d -Wl,-rpath,'$$ORIGIN' -lz -lm
+	$(CC) $(CFLAGS) -o $@ $< -L$(LIBDIR) -ldct3dcodec -ldct3d -Wl,-rpath,'$$ORIGIN' -lz -lm -lpthread
 
 oracle:
 	$(MAKE) -C oracle

@@ -306,3 +306,47 @@ def test_decoder_window_and_consume(pkg, plan8):
     assert L.dct3d_entropy_dec_window(d, 16, C.byref(p), C.byref(n), C.byref(bit)) == 0
     assert bit.value == 1 and C.string_at(p, n.value) == raw[8:]
     L.dct3d_entropy_dec_destroy(d)
+
+
+def entropy_encode_mt(pkg, q, w, h, stacks, depth, threads, chunk):
+    L = codec(pkg)
+    L.dct3d_codec_entropy_encode_mt.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_size_t,
+                                                C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    out, n = C.c_void_p(), C.c_size_t()
+    q = np.ascontiguousarray(q, np.int32)
+    assert L.dct3d_codec_entropy_encode_mt(q.ctypes.data, w, h, stacks, depth, threads, chunk, C.byref(out),
+                                           C.byref(n)) == 0
+    b = C.string_at(out, n.value)
+    L.dct3d_codec_free(out)
+    return b
+
+
+@pytest.mark.parametrize("threads,chunk", [(4, 4096), (3, 1000), (8, 0), (2, 1)])
+def test_parallel_deflate_inflates_to_reference_payload(pkg, plan8, threads, chunk):
+    """the optional parallel deflate (chunks primed with the preceding
+    32 KiB, joined by sync flushes in one zlib stream) writes a different .bin whose inflated payload
+    equals that of the reference encoder's .bin (encoder.c:73-86,136-139,266-274); the host decoder
+    reads it back to the same coefficients.  Ragged chunk sizes (1000, 1 byte) cross the stack pushes
+    and the carried partial byte."""
+    w, h, stacks = 64, 48, 3
+    fr = pkg.synthetic.frames(w, h, 8 * stacks, kind="uniform")
+    q = plan8.encode_q(fr).reshape(-1)
+    par = entropy_encode_mt(pkg, q, w, h, stacks, 8, threads, chunk)
+    single = entropy_encode(pkg, q, w, h, stacks, 8)
+    assert zlib.decompress(par) == zlib.decompress(single)
+    if chunk and chunk < len(zlib.decompress(single)):
+        assert par != single  # several chunks: not the single stream's bytes
+    rc, back = entropy_decode(pkg, par, w, h, stacks, 8)
+    assert rc == 0 and np.array_equal(back, q)
+    try:
+        ref = reference_entropy_encode(q, w, h, stacks, 8)
+    except pytest.skip.Exception:
+        return
+    assert zlib.decompress(par) == zlib.decompress(ref)
+
+
+def test_parallel_deflate_single_thread_is_reference_bytes(pkg, plan8):
+    """threads <= 1 keeps the single zlib stream: the reference encoder's .bin bytes."""
+    fr = pkg.synthetic.frames(64, 48, 16, kind="ramp")
+    q = plan8.encode_q(fr).reshape(-1)
+    assert entropy_encode_mt(pkg, q, 64, 48, 2, 8, 1, 0) == entropy_encode(pkg, q, 64, 48, 2, 8)

@@ -1,7 +1,7 @@
 """End-to-end codec timing (run on the GPU box): the reference-compatible CLI on a synthetic 1080p raw
 file, Exp-Golomb on the host (the reference's split: quantised ints over PCIe) vs on the device (only
 the stream crosses PCIe), encode and decode; both must write the same .bin / frames.  One JSON line."""
-import importlib, json, os, subprocess, sys, tempfile, time
+import importlib, json, os, subprocess, sys, tempfile, time, zlib
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -27,18 +27,33 @@ for mode in ("1", "0"):
     bins[mode] = open(out, "rb").read()
     res["encode_host_eg_s" if mode == "1" else "encode_device_eg_s"] = dt
 res["bin_identical"] = bins["0"] == bins["1"]
+# optional parallel deflate: a different .bin, the same inflated payload
+T = int(os.environ.get("E2E_DEFLATE_THREADS", "16"))
+env = dict(os.environ, DCT3D_CODEC_HOST_EG="0", DCT3D_CODEC_DEFLATE_THREADS=str(T))
+outp = os.path.join(tmp, "outp.bin")
+t0 = time.perf_counter()
+r = subprocess.run([pkg.CLI_PATH, "encode", raw, outp, str(W), str(H), str(F), "1"], capture_output=True, text=True,
+                   env=env)
+res["encode_parallel_deflate_s"] = time.perf_counter() - t0
+assert r.returncode == 0, r.stdout + r.stderr
+binp = open(outp, "rb").read()
+res["deflate_threads"] = T
+res["parallel_bin_MB"] = len(binp) / 1e6
+res["parallel_payload_identical"] = zlib.decompress(binp) == zlib.decompress(bins["0"])
+res["encode_parallel_deflate_fps"] = F / res["encode_parallel_deflate_s"]
 res["bin_MB"] = len(bins["0"]) / 1e6
 decs = {}
-for mode in ("1", "0"):
-    env = dict(os.environ, DCT3D_CODEC_HOST_EG=mode)
+for mode in ("1", "0", "p"):
+    env = dict(os.environ, DCT3D_CODEC_HOST_EG="1" if mode == "1" else "0")
+    src = os.path.join(tmp, "outp.bin" if mode == "p" else "out0.bin")
     dec = os.path.join(tmp, f"dec{mode}.raw")
     t0 = time.perf_counter()
-    r = subprocess.run([pkg.CLI_PATH, "decode", os.path.join(tmp, "out0.bin"), dec, str(W), str(H), str(F), "1"],
+    r = subprocess.run([pkg.CLI_PATH, "decode", src, dec, str(W), str(H), str(F), "1"],
                        capture_output=True, text=True, env=env)
-    res["decode_host_eg_s" if mode == "1" else "decode_s"] = time.perf_counter() - t0
+    res[{"1": "decode_host_eg_s", "0": "decode_s", "p": "decode_parallel_bin_s"}[mode]] = time.perf_counter() - t0
     assert r.returncode == 0, r.stdout + r.stderr
     decs[mode] = open(dec, "rb").read()
-res["decoded_identical"] = decs["0"] == decs["1"]
+res["decoded_identical"] = decs["0"] == decs["1"] == decs["p"]
 res["encode_device_eg_fps"] = F / res["encode_device_eg_s"]
 res["encode_host_eg_fps"] = F / res["encode_host_eg_s"]
 res["decode_fps"] = F / res["decode_s"]
