@@ -738,7 +738,9 @@ __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2
         double t = 0.0;
 #pragma unroll 1
         for (int e = 0; e < 4; e += 2) {  // two rows' chains side by side
-            uint32_t w[4] = {raw[e].x, raw[e + 1].x, raw[e].y, raw[e + 1].y};
+            // rows picked by selects, not raw[e]: a runtime index would put raw in scratch memory
+            const uint2 ra = e == 0 ? raw[0] : raw[2], rb = e == 0 ? raw[1] : raw[3];
+            uint32_t w[4] = {ra.x, rb.x, ra.y, rb.y};
             double r0 = 0.0, r1 = 0.0;
 #pragma unroll
             for (int x = 0; x < 8; x++) {
@@ -842,16 +844,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         e16_body(P, raw, wl, s_tab, lane, valid, qv, fm);
     }
     if constexpr (TRACE) t_comp = __builtin_amdgcn_s_memrealtime();
-    // ---- rare path, part 1: the second certificate's loads, issued before the stores (a load issued
-    //      after them would wait for them too: one in-order vmcnt) ----
     const bool rare = !MEM && !COMP && P.recheck && __builtin_expect(__ballot(fm != 0u) != 0ull, 0);  // wave-uniform
-    uint2 raw2[4];
-    double bv = 0.0, tv = 0.0;
-    if (rare) {
-        e16_load(P, g, valid, k, h, raw2);
-        bv = P.tab64[lane];
-        tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
-    }
 
     const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
                        P.ngroups, P.coef, P.group_of};
@@ -890,8 +883,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
             *(ulonglong2*)(tr + 2) = make_ulonglong2(t_end, ((uint64_t)xcc << 32) | hw);
         }
     }
-    // ---- rare path, part 2: the second certificate (one counter update per wave) ----
+    // ---- rare path: the second certificate (one counter update per wave).  Its loads (the rows again,
+    //      the fp64 tables) are issued after the stores: one in-order vmcnt makes them wait for the
+    //      stores too, but rows loaded before the stores and held across them spilled to scratch
+    //      (the 72-VGPR cap), which cost every wave a scratch allocation and the rare ones a wait on
+    //      the reload before their stores ----
     if (rare) {
+        uint2 raw2[4];
+        e16_load(P, g, valid, k, h, raw2);
+        const double bv = P.tab64[lane];
+        const double tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
         uint32_t nset;
         e16_recheck64(P, raw2, bv, tv, s_b64, lane, cube0, fm, nset);
         for (int o = 1; o < 64; o <<= 1) nset += __shfl_xor(nset, o, 64);

@@ -1,13 +1,21 @@
 #!/bin/bash
-# A/B of whole builds on one box: for each run in RUNS ("dir" = a tree under ab/ or "." for the
-# working tree), one bench of CONFIG (ARGS extra); prints dir / value / kernel ms per run.
+# A/B of builds on one box: ab/<side> copies (git archive + make) against the working
+# tree ("cur"), interleaved over ROUNDS rounds, for each argument set "label|bench args".
+#   SIDES="base cur" ROUNDS=2 tools/ab_dirs.sh "c2|" "c2u|--kind uniform"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-mkdir -p gpurun_out/ab
-i=0
-for d in ${RUNS:-. ab/base . ab/base}; do
-  i=$((i+1))
-  (cd $d && timeout -k 10 200 python bench.py --config ${CONFIG:-c2_encode_1080p} --steps 20 --warmup 5 --no-cpu-baseline ${ARGS}) > gpurun_out/ab/dirs_$i.log 2>&1
-  rc=$?; case $rc in 0) ;; *) echo "$d bench rc=$rc"; tail -3 gpurun_out/ab/dirs_$i.log; exit $rc;; esac
-  python3 -c "import json; r=json.loads(open('gpurun_out/ab/dirs_$i.log').read().strip().splitlines()[-1]); c=r.get('ceiling') or {}; print('$d', round(r['value']/1e9,4),'Gcubes/s ms/step', round(r['ms_per_step'],4), 'kernel_ms', round(r['roofline']['kernel_ms'],4), 'frac', round(r['roofline']['frac'],4), 'memonly', round(c.get('encode_memonly_ms',0),4))"
+OUT=$PWD/gpurun_out/${OUT:-abd}
+mkdir -p $OUT
+for i in $(seq 1 ${ROUNDS:-2}); do
+  for v in "$@"; do
+    label=${v%%|*}; args=${v#*|}
+    for side in ${SIDES:-base cur}; do
+      dir=.; [ $side != cur ] && dir=ab/$side
+      (cd $dir && timeout -k 10 180 python bench.py $args --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-ceiling) \
+         > $OUT/${label}_${side}_$i.log 2>&1
+      rc=$?; [ $rc -ne 0 ] && { tail -5 $OUT/${label}_${side}_$i.log; echo "stopping: $label $side rc=$rc"; exit $rc; }
+      tail -1 $OUT/${label}_${side}_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$label', '$side', $i, 'ms/step', round(d['ms_per_step'],4), 'kernel', round(r['kernel_ms'],4), 'frac', round(r['frac'],4), 'rechecked', d.get('rechecked_units_last_step'))"
+    done
+  done
 done
+exit 0
