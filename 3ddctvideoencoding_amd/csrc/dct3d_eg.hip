@@ -529,6 +529,13 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
 
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     __shared__ uint32_t win[kSyncWinWords];
+    // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
+    // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
+    // (status[2] != 0) and the host reruns without speculation
+    if (P.status[0] != 0) {  // grid-uniform
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned int*)&P.status[2], 4u);
+        return;
+    }
     const LdsBits L = stage_block_window(P, win);
     const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (t >= P.n_chunks) return;

@@ -67,6 +67,7 @@ struct dct3d_ctx {
     bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
     uint32_t opt_enc_stagger = 0;
+    bool opt_eg_force_retry = false;
     int n_cus = 0, enc_layers = 0;  // device CUs, resident encode16 blocks per CU (for the start stagger)
     // certify-or-replay state
     uint64_t last_units = 0;
@@ -295,6 +296,7 @@ int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_ENC_STAGGER: c->opt_enc_stagger = (uint32_t)value; return DCT3D_OK;
+        case DCT3D_OPT_EG_FORCE_RETRY: c->opt_eg_force_retry = value != 0.0; return DCT3D_OK;
         default: return DCT3D_EINVAL;
     }
 }
@@ -941,9 +943,14 @@ int dct3d_eg_fetch(dct3d_ctx* c, uint8_t* out, uint64_t nbytes) {
 // Stream decode front: sync passes until the chunk exits converge, the scan of per-chunk code counts,
 // the mark pass (bit position of every 32nd value).  No host wait after the last pass; the caller's
 // consumer kernel (emit / fused decode) skips itself on a corrupt or short stream, and eg_decode_status
-// reports it.
+// reports it.  spec (with resolve): no host wait after pass 0 either -- the scan, the mark pass and the
+// consumer are enqueued behind it at once; the mark pass reads the pass's verdict (status[0]) first and,
+// should a chunk not have resolved (never seen on encoder output), writes no marks and flags status[2]
+// bit 4, the consumer skips itself, and eg_decode_status asks the caller to rerun without speculation
+// (kEgRetry).  This takes the host round trip between pass 0 and the scan off every call.
+constexpr int kEgRetry = 1000;
 static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t start_bit, uint64_t n_cubes,
-                           EgDecParams& D) {
+                           EgDecParams& D, bool spec) {
     const uint64_t limit = nbytes * 8;
     const uint64_t n_chunks = (limit - start_bit + kEgChunkBits - 1) / kEgChunkBits;
     const uint64_t n_scan = (n_chunks + 4095) / 4096;
@@ -979,6 +986,12 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
         if (launch_eg_sync(D, (int)(it < 2 ? it : 1), resolve, c->stream)) return DCT3D_EKERNEL;
         cur ^= 1;
         if (it == 0 && !resolve) continue;
+        if (it == 0 && spec) {  // the verdict is read on the device (eg_mark_kernel)
+            // test option: a failed verdict, to exercise the skip-and-rerun path
+            if (c->opt_eg_force_retry && hipMemsetAsync(c->d_egd_status.p, 0x01, 1, c->stream) != hipSuccess)
+                return DCT3D_EDEVICE;
+            break;
+        }
         uint64_t changed = 0;
         if (hipMemcpyAsync(&changed, c->d_egd_status.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
@@ -1009,6 +1022,7 @@ static int eg_decode_status(dct3d_ctx* c, const EgDecParams& D, uint64_t* end_bi
         hipMemcpyAsync(total, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return DCT3D_EDEVICE;
+    if (st[2] & 4) return kEgRetry;  // a speculative front whose pass 0 did not resolve: rerun
     if (st[2] & 1) return DCT3D_EINVAL;
     if ((st[2] & 2) || total[0] < D.n_values) return DCT3D_ENODATA;
     if (end_bit) *end_bit = st[1];
@@ -1022,12 +1036,15 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (end_bit) *end_bit = start_bit;
     if (n_cubes == 0) return DCT3D_OK;
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
-    EgDecParams D;
-    int rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, D);
-    if (rc) return rc;
-    D.q = d_q;
-    if (launch_eg_emit(c->bd, D, c->stream)) return DCT3D_EKERNEL;
-    return eg_decode_status(c, D, end_bit);
+    for (int spec = 1;; spec = 0) {
+        EgDecParams D;
+        int rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, D, spec && !c->opt_eg_no_resolve);
+        if (rc) return rc;
+        D.q = d_q;
+        if (launch_eg_emit(c->bd, D, c->stream)) return DCT3D_EKERNEL;
+        rc = eg_decode_status(c, D, end_bit);
+        if (rc != kEgRetry || !spec) return rc == kEgRetry ? DCT3D_EDEVICE : rc;
+    }
 }
 
 // Fused stream -> raster decode of stacks [st0, st0 + ns) after eg_decode_front: the decode kernel parses
@@ -1084,10 +1101,13 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (end_bit) *end_bit = start_bit;
     if (n_cubes == 0) return DCT3D_OK;
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
-    EgDecParams E;
-    if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E))) return rc;
-    if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
-    return eg_decode_status(c, E, end_bit);
+    for (int spec = 1;; spec = 0) {
+        EgDecParams E;
+        if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E, spec && !c->opt_eg_no_resolve))) return rc;
+        if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
+        rc = eg_decode_status(c, E, end_bit);
+        if (rc != kEgRetry || !spec) return rc == kEgRetry ? DCT3D_EDEVICE : rc;
+    }
 }
 
 int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int start_bit, int w, int h, int n_stacks,
@@ -1102,17 +1122,22 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if ((uint64_t)start_bit >= nbytes * 8) return DCT3D_ENODATA;
     if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3))) return rc;
     if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    EgDecParams E;
-    if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E))) return rc;
-    // the raster leaves in chunks of stacks while the next chunk decodes (the stream is small: no upload)
-    const size_t px = n_cubes * c->plan.cs / n_stacks;
-    batch_begin(c);
-    rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
-        return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
-    });
-    batch_end(c);
-    if (rc) return rc;
-    return eg_decode_status(c, E, end_bit);
+    for (int spec = 1;; spec = 0) {
+        EgDecParams E;
+        if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E,
+                                  spec && !c->opt_eg_no_resolve)))
+            return rc;
+        // the raster leaves in chunks of stacks while the next chunk decodes (the stream is small: no upload)
+        const size_t px = n_cubes * c->plan.cs / n_stacks;
+        batch_begin(c);
+        rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
+            return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
+        });
+        batch_end(c);
+        if (rc) return rc;
+        rc = eg_decode_status(c, E, end_bit);
+        if (rc != kEgRetry || !spec) return rc == kEgRetry ? DCT3D_EDEVICE : rc;
+    }
 }
 
 }  // extern "C"

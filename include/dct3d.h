@@ -128,6 +128,8 @@ int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_s
                                          coefficient the fp32 certificate leaves open takes the Java fold */
 #define DCT3D_OPT_EG_TWO_STEP 5       /* 1: dct3d_encode_eg / dct3d_decode_eg through int32 cubes */
 #define DCT3D_OPT_EG_NO_RESOLVE 6     /* 1: Exp-Golomb decode sync by plain confirming passes only */
+#define DCT3D_OPT_EG_FORCE_RETRY 8    /* test: the Exp-Golomb decode's speculative front reports an unresolved
+                                         pass 0, so the call takes its skip-and-rerun path (same results) */
 #define DCT3D_OPT_ENC_STAGGER 7       /* 8x8x8 encode: start stagger of the first resident round, in units of
                                          512 cycles per resident layer (0 = off); results are unchanged */
 int dct3d_ctx_set_option(dct3d_ctx *ctx, int option, double value);

@@ -255,3 +255,27 @@ def test_fused_decode_dense_long_codes(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_
     got, eb = _decode_fused(ctx, data, 64, 48, 2)
     assert eb == nbits
     assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
+
+
+def test_speculative_front_rerun_on_unresolved_pass0(pkg, oracle, plan8, gpu_ctx8):
+    """The stream decode enqueues its scan, mark pass and consumer right behind the resolving sync pass
+    (no host round trip); should pass 0 not resolve, the mark pass writes nothing, the consumer skips
+    itself and the call reruns without speculation.  DCT3D_OPT_EG_FORCE_RETRY forces that verdict: the
+    three entry points (two-step, fused device, fused host) give the same results and errors."""
+    fr = pkg.synthetic.frames(128, 64, 24, kind="uniform", frame0=4)
+    q = plan8.encode_q(fr)
+    data, nbits = _expected(oracle, pkg, q, 8)
+    ref_fused, eb0 = _decode_fused(gpu_ctx8, data, 128, 64, 3)
+    ref_two, eb1 = _decode_two_step(gpu_ctx8, data, 128, 64, 3)
+    ref_host, eb2 = gpu_ctx8.decode_eg(data, 128, 64, 3)
+    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_FORCE_RETRY, 1):
+        got_fused, e0 = _decode_fused(gpu_ctx8, data, 128, 64, 3)
+        got_two, e1 = _decode_two_step(gpu_ctx8, data, 128, 64, 3)
+        got_host, e2 = gpu_ctx8.decode_eg(data, 128, 64, 3)
+        with pytest.raises(pkg.Dct3dError) as e:
+            _decode_fused(gpu_ctx8, data[: len(data) // 2], 128, 64, 3)
+        assert e.value.code == pkg.DCT3D_ENODATA
+    assert eb0 == eb1 == e0 == e1 == nbits and eb2 == e2
+    expect = plan8.decode_q(q, 128, 64, 24)
+    for got in (ref_fused, ref_two, ref_host, got_fused, got_two, got_host):
+        assert np.array_equal(got, expect)
