@@ -30,7 +30,7 @@ INCLUDE_DIR = os.path.join(REPO_DIR, "include")
 DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC, DCT3D_ENODATA = 0, 1, 2, 3, 4, 5, 6
 # test / diagnostic options (include/dct3d.h, Context.set_option)
 DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 2, 3, 5, 6
-DCT3D_OPT_ENC_STAGGER, DCT3D_OPT_EG_FORCE_RETRY = 7, 8
+DCT3D_OPT_EG_FORCE_RETRY = 8
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (

@@ -817,11 +817,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
         // a starting wave computes its addresses and issues its loads at the top priority: under the
         // default oldest-first issue they queue behind the computing waves' VALU work, and a box whose
         // encode loses the overlap of memory and compute that way runs 10 % slower (variant_sweep.txt)
-        if constexpr (!MEM && !COMP) {
-            if (P.stagger && blockIdx.x < P.stagger_cus * P.stagger_layers) {
-                for (uint32_t i = (blockIdx.x / P.stagger_cus) * P.stagger; i; i--) __builtin_amdgcn_s_sleep(8);
-            }
-        }
         if constexpr (!MEM) __builtin_amdgcn_s_setprio(3);
         e16_load(P, g, valid, k, h, raw);
         if constexpr (!MEM) __builtin_amdgcn_s_setprio(0);

@@ -45,10 +45,6 @@ struct EncodeParams {
     unsigned int* replay_clear;  // the other slot (2S words): zeroed by block 0 for the next call
     const double* tab64;       // 8x8x8 second certificate: [64] fp64 basis [k][n], [32] thresholds per s
     uint32_t recheck;          // 1: run the second certificate (0: test option, all open -> Java fold)
-    // start stagger of the first resident round (8x8x8): block b < stagger_cus * stagger_layers waits
-    // (b / stagger_cus) * stagger x 512 cycles before its loads, so that the resident blocks of a CU do
-    // not load, compute and store in lockstep (0: off)
-    uint32_t stagger, stagger_cus, stagger_layers;
     uint64_t* trace;           // MODE 3 (diagnostic timeline): per wave {start, transform done, stored, hw id}
 };
 
@@ -78,8 +74,6 @@ struct Fwd64Params {
 int launch_cube_f32(int D, bool inverse, const float* in, float* out, uint32_t n_cubes, hipStream_t st);
 int launch_fwd64_raster(int D, const Fwd64Params& P, hipStream_t st);
 int launch_encode(int D, const EncodeParams& P, hipStream_t st);
-// CUs of the device and resident encode16_kernel blocks per CU
-int encode_occupancy(int device, int* n_cus, int* blocks_per_cu);
 struct EgParams {
     const int32_t* q;          // cube-major quantised values
     uint64_t n_cubes;

@@ -479,16 +479,6 @@ int launch_encode(int D, const EncodeParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int encode_occupancy(int device, int* n_cus, int* blocks_per_cu) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, encode16_kernel<true, 0>, kBlock, 0) != hipSuccess) return -1;
-    *n_cus = prop.multiProcessorCount;
-    *blocks_per_cu = nb;
-    return 0;
-}
-
 int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     if (D == 8) launch_enc_eg_t<8>(P, E, st);

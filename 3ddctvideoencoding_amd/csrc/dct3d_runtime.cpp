@@ -66,9 +66,7 @@ struct dct3d_ctx {
     double opt_dec_margin = 0.0;    // added to the decode margin
     bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
-    uint32_t opt_enc_stagger = 0;
     bool opt_eg_force_retry = false;
-    int n_cus = 0, enc_layers = 0;  // device CUs, resident encode16 blocks per CU (for the start stagger)
     // certify-or-replay state
     uint64_t last_units = 0;
     bool last_valid = false;
@@ -295,7 +293,6 @@ int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
         case DCT3D_OPT_ENC_NO_RECHECK: c->opt_enc_no_recheck = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
-        case DCT3D_OPT_ENC_STAGGER: c->opt_enc_stagger = (uint32_t)value; return DCT3D_OK;
         case DCT3D_OPT_EG_FORCE_RETRY: c->opt_eg_force_retry = value != 0.0; return DCT3D_OK;
         default: return DCT3D_EINVAL;
     }
@@ -477,12 +474,6 @@ int dct3d_encode_stacks_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h,
     set_count_slot(c, P.replay_count, P.replay_clear);
     P.tab64 = (const double*)c->d_tabs64.p;
     P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
-    if (c->opt_enc_stagger && D == 8) {
-        if (!c->n_cus && encode_occupancy(c->device, &c->n_cus, &c->enc_layers)) return DCT3D_EDEVICE;
-        P.stagger = c->opt_enc_stagger;
-        P.stagger_cus = (uint32_t)c->n_cus;
-        P.stagger_layers = (uint32_t)c->enc_layers;
-    }
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
     if (launch_encode(D, P, c->stream)) return DCT3D_EKERNEL;

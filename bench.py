@@ -98,8 +98,6 @@ def parse():
     ap.add_argument("--kernel-events", default="separate", choices=["separate", "timed"],
                     help="where the library's per-launch events (kernel_ms) run: a separate pass after the timed "
                          "region (default) or inside it (adds their device cost to every step)")
-    ap.add_argument("--pad-mb", type=int, default=0,
-                    help="A/B: allocate this many MiB between the input and the output buffer (placement study)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="A/B knob: a context option (DCT3D_OPT_<NAME>, dct3d_ctx_set_option) set before the run; "
                          "options change how results are reached, never the results")
@@ -358,7 +356,6 @@ def main():
     frames = torch.empty((max(1, stacks) * depth, height, width), dtype=torch.uint8, device="cuda")
     # each rank encodes different content (its own slice of one long synthetic video)
     ctx.fill_synthetic_dev(frames, width, height, stacks * depth, frame0=first * depth, kind=a.kind)
-    pad = torch.empty((a.pad_mb << 20,), dtype=torch.uint8, device="cuda") if a.pad_mb else None  # A/B: placement
     q = torch.empty((max(1, n_cubes) * cs,), dtype=torch.int32, device="cuda")
     eg_info = {}
     if direction == "decode":

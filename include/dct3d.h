@@ -130,8 +130,6 @@ int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_s
 #define DCT3D_OPT_EG_NO_RESOLVE 6     /* 1: Exp-Golomb decode sync by plain confirming passes only */
 #define DCT3D_OPT_EG_FORCE_RETRY 8    /* test: the Exp-Golomb decode's speculative front reports an unresolved
                                          pass 0, so the call takes its skip-and-rerun path (same results) */
-#define DCT3D_OPT_ENC_STAGGER 7       /* 8x8x8 encode: start stagger of the first resident round, in units of
-                                         512 cycles per resident layer (0 = off); results are unchanged */
 int dct3d_ctx_set_option(dct3d_ctx *ctx, int option, double value);
 /* Enable HIP-event timing of the kernels (reported by dct3d_get_stats). */
 int dct3d_ctx_set_profiling(dct3d_ctx *ctx, int on);
