@@ -105,6 +105,7 @@ static void *pz_worker(void *arg) {
                 j->out_len = cap - zs.avail_out;
                 if (rc == Z_STREAM_ERROR) err = 1;
                 else if (j->last ? rc == Z_STREAM_END : (zs.avail_in == 0 && zs.avail_out != 0)) break;
+                else if (rc == Z_BUF_ERROR && zs.avail_out != 0) err = 1;  /* no progress possible */
                 else if (zs.avail_out == 0) {  /* grow and continue */
                     unsigned char *o = (unsigned char *)realloc(j->out, cap * 2);
                     if (!o) err = 1;
