@@ -532,9 +532,14 @@ __device__ __forceinline__ int exact_coef(const ReplayGeom& R, uint32_t g, uint3
 constexpr int kE16CPW = 4;     // cubes per wave
 constexpr int kE16TZ = 144;    // transpose: kz stride (4 y x 16 B per h, 2 h, + 16 B: bank spread)
 constexpr int kE16TC = 8 * kE16TZ;
-constexpr int kE16SC = 8 * kFace;  // output staging: cube stride (faces of 256 + 16 B)
 constexpr int kE16Lds = 4 * kE16TC;
-static_assert(kE16Lds >= 2 * kE16SC, "two staged cubes per round");
+// int16 staging of all 4 cubes at once (|q| <= 255 sqrt(512) < 2^15 by Parseval, DC included): face of
+// 8 rows x 8 values (128 B) + 16 B bank spread, so the second certificate settles its coefficients in LDS
+// before any store is issued.  (int32 staging, two cubes per round, with the recheck after the stores:
+// c2 uniform 2.043 -> 2.018 ms, c2 1.883 -> 1.870 ms; profiles/r03/variant_sweep.txt)
+constexpr int kE16S16F = 144;
+constexpr int kE16S16C = 8 * kE16S16F;
+static_assert(4 * kE16S16C <= kE16Lds, "int16 staging of the wave's 4 cubes fits its region");
 
 // rows of the lane's cube (row y = k of frames 4h .. 4h + 3), zero past the end
 __device__ __forceinline__ void e16_load(const EncodeParams& P, uint32_t g, bool valid, int k, int h, uint2 (&raw)[4]) {
@@ -710,15 +715,15 @@ __device__ __forceinline__ void e16_flag_pos(uint32_t fm, int src, uint32_t cube
 // q64 = v64 / step is settled iff |q64 - rint(q64)| < thr64[s]: then Math.round of Java's value is
 // rint(q64) (bound: dct3d_plan.cpp, "second certificate").  What stays open is returned in fm for the
 // exact Java fold; nset counts the settled ones (owner lanes).
-// Timing: the rows (raw, again: L2) and the tables (bv, tv) were loaded before the wave's stores and
-// arrive while those drain; this runs after the stores, and the owning lane writes a settled value
-// over the provisional one once the wave's stores are complete (vmcnt(0): the same word was stored by
-// another lane of the wave).  Register pressure stays with the main path's 72 VGPRs.  s_b: the block's
-// copy of the tables ([64] basis, [32] thresholds), written by every wave that takes this path
-// (identical bits) and read only after its own writes.
+// Timing: it runs after the wave's cubes are staged as int16 in LDS and before any store is issued, so
+// its row reload (L2) waits for nothing but itself; the owning lane writes a settled value over the
+// provisional one in the staging (wl).  Register pressure stays with the main path's 72 VGPRs (the
+// staged values are out of the registers by then).  s_b: the block's copy of the tables ([64] basis,
+// [32] thresholds), written by every wave that takes this path (identical bits) and read only after its
+// own writes.
 __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2 (&raw)[4], double bv, double tv,
-                                              double* s_b, int lane, uint32_t cube0, uint32_t& fm, uint32_t& nset) {
-    constexpr int CS = 512;
+                                              double* s_b, char* wl, int lane, uint32_t cube0, uint32_t& fm,
+                                              uint32_t& nset) {
     const int k = lane & 7, h = (lane >> 4) & 1;
     s_b[lane] = bv;
     if (lane < 32) s_b[64 + lane] = tv;
@@ -766,9 +771,8 @@ __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2
             const double q = __ddiv_rn(t, (double)(5 * s));  // s >= 1: the DC is never open
             const double n = __builtin_rint(q);
             if (__builtin_fabs(q - n) < s_b[64 + s]) {
-                const uint32_t cube = cube0 + (lane >> 5) * 2 + ((lane & 15) >> 3);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                P.out[(size_t)cube * CS + (kz * 8 + ky) * 8 + kx] = (int32_t)n;
+                const uint32_t cl = (lane >> 5) * 2 + ((lane & 15) >> 3);  // the cube within the wave
+                *(int16_t*)(wl + cl * kE16S16C + kz * kE16S16F + (ky * 8 + kx) * 2) = (int16_t)n;  // int16 staging
                 nset++;
             } else {
                 open |= 1u << bit;
@@ -788,8 +792,8 @@ __device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2
 // issue work alone.
 // One launch is the whole encode: no flag list, no counter reset, no fixup launch.  Block 0 zeroes the
 // next call's counter slot (P.replay_clear; the two slots alternate between calls).  7 waves per SIMD
-// (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (they
-// spill a few registers to scratch instead, off the main path).
+// (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (the
+// kernel needs no scratch: tools/isa_count.py).
 static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the wave's region");
 template <bool NT, int MODE = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void encode16_kernel(EncodeParams P) {
@@ -844,30 +848,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
                        P.ngroups, P.coef, P.group_of};
 
-    // ---- stage two cubes per round (lanes 0-31: cubes 0, 1; lanes 32-63: cubes 2, 3), 1 KiB stores ----
-#pragma unroll
-    for (int rd = 0; rd < 2; rd++) {
-        if ((lane >> 5) == rd) {
-            char* dst = wl + (c & 1) * kE16SC + k * kFace + h * 16;
+    {
+        // ---- all 4 cubes staged as int16 at once; the second certificate settles its coefficients in
+        //      this staging (its row reload waits for nothing but itself: no store has been issued yet);
+        //      then 8 stores of 1 KiB, each lane's 4 int16 widened to 16 B ----
+        {
+            char* dst = wl + c * kE16S16C + k * kE16S16F + h * 8;
 #pragma unroll
             for (int ky = 0; ky < 8; ky++)
-                *(int4*)(dst + ky * 32) = make_int4(qv[ky][0], qv[ky][1], qv[ky][2], qv[ky][3]);
+                *(uint2*)(dst + ky * 16) = make_uint2(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
+                                                      __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u));
         }
         wave_lds_sync();
-        const uint32_t rcube0 = cube0 + 2 * rd;
-        char* outb = (char*)(P.out + (size_t)rcube0 * CS);
+        if (rare) {
+            uint2 raw2[4];
+            e16_load(P, g, valid, k, h, raw2);
+            const double bv = P.tab64[lane];
+            const double tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
+            uint32_t nset;
+            e16_recheck64(P, raw2, bv, tv, s_b64, wl, lane, cube0, fm, nset);
+            for (int o = 1; o < 64; o <<= 1) nset += __shfl_xor(nset, o, 64);
+            if (lane == 0 && nset && P.replay_count)
+                atomicAdd(P.replay_count + kCountSpread + (blockIdx.x & (kCountSpread - 1)), nset);
+        }
+        char* outb = (char*)(P.out + (size_t)cube0 * CS);
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int q = t * 64 + lane;  // 16-byte chunk of the round's two cubes
+        for (int t = 0; t < 8; t++) {
+            const int q = t * 64 + lane;  // 16-byte output chunk of the wave's 4 cubes (4 values)
             const int cc = q >> 7, face = (q >> 4) & 7, w = q & 15;
-            if (rcube0 + cc < P.n_cubes && (!COMP || P.width == 0u)) {
-                const int4 v = *(const int4*)(wl + cc * kE16SC + face * kFace + w * 16);
-                store16<NT>(outb + (size_t)q * 16, v);
+            if (cube0 + cc < P.n_cubes && (!COMP || P.width == 0u)) {
+                const uint2 v = *(const uint2*)(wl + cc * kE16S16C + face * kE16S16F + w * 8);
+                store16<NT>(outb + (size_t)q * 16, make_int4((int)(int16_t)v.x, (int)v.x >> 16, (int)(int16_t)v.y,
+                                                             (int)v.y >> 16));
             }
         }
         wave_lds_sync();
     }
-
     if constexpr (TRACE) {  // the wave's timeline: start, transform done, stores issued (+ 100 MHz clock)
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_ID
@@ -877,22 +893,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
             *(ulonglong2*)tr = make_ulonglong2(t_start, t_comp);
             *(ulonglong2*)(tr + 2) = make_ulonglong2(t_end, ((uint64_t)xcc << 32) | hw);
         }
-    }
-    // ---- rare path: the second certificate (one counter update per wave).  Its loads (the rows again,
-    //      the fp64 tables) are issued after the stores: one in-order vmcnt makes them wait for the
-    //      stores too, but rows loaded before the stores and held across them spilled to scratch
-    //      (the 72-VGPR cap), which cost every wave a scratch allocation and the rare ones a wait on
-    //      the reload before their stores ----
-    if (rare) {
-        uint2 raw2[4];
-        e16_load(P, g, valid, k, h, raw2);
-        const double bv = P.tab64[lane];
-        const double tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
-        uint32_t nset;
-        e16_recheck64(P, raw2, bv, tv, s_b64, lane, cube0, fm, nset);
-        for (int o = 1; o < 64; o <<= 1) nset += __shfl_xor(nset, o, 64);
-        if (lane == 0 && nset && P.replay_count)
-            atomicAdd(P.replay_count + kCountSpread + (blockIdx.x & (kCountSpread - 1)), nset);
     }
 
     // ---- rarest path: the exact Java fold of every coefficient both certificates left open (exact
