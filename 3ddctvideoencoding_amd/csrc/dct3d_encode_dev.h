@@ -721,9 +721,8 @@ __device__ __forceinline__ void e16_flag_pos(uint32_t fm, int src, uint32_t cube
 // staged values are out of the registers by then).  s_b: the block's copy of the tables ([64] basis,
 // [32] thresholds), written by every wave that takes this path (identical bits) and read only after its
 // own writes.
-__device__ __forceinline__ void e16_recheck64(const EncodeParams& P, const uint2 (&raw)[4], double bv, double tv,
-                                              double* s_b, char* wl, int lane, uint32_t cube0, uint32_t& fm,
-                                              uint32_t& nset) {
+__device__ __forceinline__ void e16_recheck64(const uint2 (&raw)[4], double bv, double tv, double* s_b, char* wl,
+                                              int lane, uint32_t& fm, uint32_t& nset) {
     const int k = lane & 7, h = (lane >> 4) & 1;
     s_b[lane] = bv;
     if (lane < 32) s_b[64 + lane] = tv;
@@ -866,7 +865,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
             const double bv = P.tab64[lane];
             const double tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
             uint32_t nset;
-            e16_recheck64(P, raw2, bv, tv, s_b64, wl, lane, cube0, fm, nset);
+            e16_recheck64(raw2, bv, tv, s_b64, wl, lane, fm, nset);
             for (int o = 1; o < 64; o <<= 1) nset += __shfl_xor(nset, o, 64);
             if (lane == 0 && nset && P.replay_count)
                 atomicAdd(P.replay_count + kCountSpread + (blockIdx.x & (kCountSpread - 1)), nset);
