@@ -78,7 +78,7 @@ struct dct3d_ctx {
     int enc_slot = 0;
     int last_count_slot = -1;  // >= 0: the last call's statistics are in d_enc_counts[slot]
     bool slot_used = false;    // a counting kernel of the current call was enqueued into enc_slot
-    bool batch = false;        // a host entry point's chunks: one slot for the whole call (close_slot after)
+    bool batch = false;        // a host entry point's chunks: one slot for the whole call (batch_end flips it)
     uint64_t batch_units = 0;
     hipEvent_t ev_switch = nullptr;  // orders a dct3d_ctx_set_stream switch after the old stream's work
     // host-pointer entry point staging
