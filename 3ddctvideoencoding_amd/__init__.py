@@ -31,6 +31,7 @@ DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC
 # test / diagnostic options (include/dct3d.h, Context.set_option)
 DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 2, 3, 5, 6
 DCT3D_OPT_EG_FORCE_RETRY = 8
+DCT3D_OPT_EG_DEC_GROUPS = 9
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (

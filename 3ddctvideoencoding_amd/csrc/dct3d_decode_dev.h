@@ -235,7 +235,9 @@ __device__ __forceinline__ int dec_cube_of_lane(int lane) { return (lane >> 5) *
 // a wave instruction covering 1 KiB of whole 128-byte lines.  Per-lane 4- or 8-byte row pieces cost
 // ~1.5x the write time (profiles/r02/variant_sweep.txt).  Other blocks store per lane.  Every wave of
 // the block must call this (the barrier); a full block has no early-returning wave.
-template <int D>
+// LOOP: called inside a caller's loop (decode_eg_kernel's groups): the lane's addresses are made here, not
+// hoisted out of the loop and held across the transform.
+template <int D, bool LOOP = false>
 __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
                                                const uint32_t (&outw)[D][(D == 8) ? 1 : 2], bool valid) {
     using G = DecGeom<D>;
@@ -258,6 +260,8 @@ __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, 
         __syncthreads();
         const char* lds0 = wl - wave * kDecWaveLds;
         constexpr int CPR = kWavesPerBlock * W / 16;  // 16-byte chunks per block row
+        int tid = (int)threadIdx.x;
+        if constexpr (LOOP) asm volatile("" : "+v"(tid));
         // the block's first cube, wave-uniform (scalar arithmetic); a block inside one block-row (every
         // block when nbx is a multiple of 4 CPW) addresses its chunks from it directly
         const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk0);
@@ -268,7 +272,7 @@ __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, 
         uint8_t* const base0 = P.out + (size_t)s0 * P.stack_stride + (size_t)(by0 * 8) * P.width + bx0 * 8;
 #pragma unroll
         for (int i = 0; i < D * 8 * CPR / kBlock; i++) {
-            const int q = (int)threadIdx.x + kBlock * i;
+            const int q = tid + kBlock * i;
             const int z = q / (8 * CPR), r = q % (8 * CPR), yy = r / CPR, j = r % CPR;
             const int4 v = *(const int4*)(lds0 + (j * 16 / W) * kDecWaveLds + z * 8 * W + yy * W + (j * 16) % W);
             uint8_t* dst;
@@ -301,7 +305,7 @@ __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, 
 // once the staged input is in registers (the persistent variant issues the next tile's loads there);
 // reload(g, cf, lane) re-reads cube g's dequantised coefficients for the rare exact replay.
 // PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
-template <int D, int PG, class AfterA, class Reload>
+template <int D, int PG, bool LOOP = false, class AfterA, class Reload>
 __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
                                             AfterA&& after_a, const Reload& reload) {
     using G = DecGeom<D>;
@@ -322,7 +326,8 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     double b[8][4];
     float l1_f;
     {
-        const int sb = 5 * (4 * h + k);                     // step = sb + 5 (e + ky); DC (e = ky = 0): 1
+        int sb = 5 * (4 * h + k);  // step = sb + 5 (e + ky); DC (e = ky = 0): 1
+        if constexpr (LOOP) asm volatile("" : "+v"(sb));  // (dec_store_tile's LOOP)
         double stp[11];
         stp[0] = (double)max(sb, 1);
 #pragma unroll
@@ -485,7 +490,7 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
         if (lane == 0 && P.replay_count) atomicAdd(P.replay_count + (blockIdx.x & (kCountSpread - 1)), nrep);
     }
     __builtin_amdgcn_s_setprio(2);  // the store phase ahead of the computing waves (as encode16_kernel)
-    dec_store_tile<D>(P, wl, lane, cube0, outw, valid);
+    dec_store_tile<D, LOOP>(P, wl, lane, cube0, outw, valid);
 }
 
 // Block 0 zeroes the next call's counter slot, both halves (the two slots alternate between the

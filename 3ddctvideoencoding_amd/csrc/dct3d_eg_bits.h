@@ -234,8 +234,11 @@ __device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader
 // fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin)); else
 // the parse reads the stream in global memory -- a wave whose 2,048 values average more than the window
 // holds (|q| >= 2^13 nearly everywhere: never written by an encoder of 8-bit frames, but a valid stream).
+// That path's values pass through the (then unused) window region, lane-private rows of N words (64 N
+// words: every caller's region holds them), so that v is written at constant indices only (a runtime index into v would make a caller's loop carry
+// all of v: decode_eg_kernel).
 template <int N>
-__device__ __forceinline__ void parse_values(const EgDecParams& P, const uint32_t* win, uint32_t nwin, uint64_t w0,
+__device__ __forceinline__ void parse_values(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
                                              bool fits, uint64_t my, int32_t (&v)[N]) {
     if (fits) {
         ValidWinReader r{win, 0, 0, 0, 0, 0};
@@ -243,14 +246,16 @@ __device__ __forceinline__ void parse_values(const EgDecParams& P, const uint32_
 #pragma unroll
         for (int i = 0; i < N; i++) v[i] = eg_value_fast(r.get());
     } else {
+        int32_t* row = (int32_t*)win + (threadIdx.x & 63) * N;
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
         r.seek(my);
-#pragma unroll 4
         for (int i = 0; i < N; i++) {
             uint32_t code = 1u;
             (void)r.get(code);
-            v[i] = eg_value(code);
+            row[i] = eg_value(code);
         }
+#pragma unroll
+        for (int i = 0; i < N; i++) v[i] = row[i];
     }
 }
 

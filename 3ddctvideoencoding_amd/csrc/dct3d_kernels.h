@@ -141,6 +141,7 @@ int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mar
 int launch_eg_mark(const EgDecParams& P, hipStream_t st);
 int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st);
 // fused stream -> raster decode: values parsed at the marks straight into the decode's LDS staging
-int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st);
+// groups_per_wave: 1, 2, 4 or 8 (other values: 8) groups of CPW cubes per wave, the next one's loads ahead
+int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, int groups_per_wave, hipStream_t st);
 
 }  // namespace dct3d

@@ -378,15 +378,31 @@ struct ReloadStream {
     }
 };
 
-template <int D>
+// lane 0's 64-bit value in scalar registers (readfirstlane returns int: widened from uint32_t, unsigned)
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// NG groups per wave (a group = the wave's CPW cubes = 64 marks), the block's 4 waves on 4 consecutive
+// groups per round (dec_store_tile's block stores).  The next group's marks are loaded while this
+// group's window is parsed, and its window words (NWP per lane, as far as they reach) while this group
+// is transformed, so the mark -> window -> parse chain of global round trips is paid once per wave, not
+// once per group.  Carried across the transform: the NWP words, the lane's mark relative to the window
+// (32 bits) and two wave-uniform 64-bit values (scalar registers).  NG = 1: no look-ahead.
+template <int D, int NG>
 __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, EgDecParams E) {
     using G = DecGeom<D>;
     constexpr uint32_t CS = G::CS, PARTS = CS / 32, CPW = G::CPW;
     static_assert(CPW * CS == 2048 && PARTS * CPW == 64, "one wave = 64 marks");
+    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,304 words >= 2,048 values x 27 bits
+    constexpr int NWP = 4;                     // window words per lane loaded ahead (256: 4 bits per value)
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];
     dec_clear_next_slot(P);
-    if (E.status[2] != 0) return;  // corrupt / short stream: reported by the mark pass (block-uniform)
+    // corrupt / short / empty stream: reported by the mark pass (block-uniform)
+    if (E.status[2] != 0 || E.n_words == 0) return;
     {  // both loads in flight before the LDS writes
         static_assert(CS % kBlock == 0, "whole passes");
         uint16_t t[CS / kBlock];
@@ -396,57 +412,90 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         for (uint32_t r = 0; r < CS / kBlock; r++) s_diag[threadIdx.x + r * kBlock] = t[r];
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    const uint32_t cube0 = P.cube_base + (xcd_tile() * kWavesPerBlock + wave) * CPW;
-    if (cube0 >= P.n_cubes) return;
-    const uint64_t n_marks = E.n_values / 32;
-    const uint64_t m0 = (uint64_t)cube0 * CS / 32;
-    __builtin_amdgcn_s_setprio(3);  // marks and window loads ahead of the computing waves
-    const bool lv = m0 + lane < n_marks;
-    const uint64_t my = lv ? E.mark[m0 + lane] : 0;
-    const uint64_t first = __shfl(my, 0, 64);
-    const uint64_t last = m0 + 64 < n_marks ? E.mark[m0 + 64] : E.status[1];  // wave-uniform
-    const uint64_t w0 = first >> 5;
-    const uint64_t span = (last >> 5) + 4 - w0;
-    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,304 words >= 2,048 values x 27 bits
-    const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_values)
-    const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* win = (uint32_t*)wl;
-    // 4 words per lane per round, all loads issued before the first LDS write: a one-word loop waited
-    // out a full global round trip per 64 words (3 for ramp content, 6+ for noise)
-    // (an empty stream never gets here: the mark pass reported it, status[2]; the guard keeps the
-    // clamped index below in range regardless, outside the loop so the loads stay unconditional)
-    const uint32_t nst = E.n_words ? nwin : 0u;
-    for (uint32_t i0 = 0; i0 < nst; i0 += 256) {
-        uint32_t t[4];
+    const uint64_t n_marks = E.n_values / 32;
+    const uint32_t row0 = xcd_tile() * NG;  // the block's first round of 4 groups
+    auto cube_of = [&](int i) { return P.cube_base + ((row0 + (uint32_t)i) * kWavesPerBlock + wave) * CPW; };
+    // the group's marks: the lane's (value 32 * (m0 + lane)) and the end of its bit range (all lanes alike)
+    auto load_marks = [&](int lane, uint32_t cube0, uint64_t& my, uint64_t& last) {
+        const uint64_t m0 = (uint64_t)cube0 * CS / 32;
+        my = m0 + lane < n_marks ? E.mark[m0 + lane] : 0;
+        last = m0 + 64 < n_marks ? E.mark[m0 + 64] : E.status[1];
+    };
+    // window of a group: first word w0 (the first mark's), the lane's mark relative to bit 32 w0, the
+    // words up to the end mark (+4 slack); its first NWP * 64 words requested (clamped into the stream)
+    auto open_window = [&](int lane, uint64_t my, uint64_t last, uint64_t& w0, uint32_t& rel, uint64_t& span,
+                           uint32_t (&t)[NWP]) {
+        w0 = uniform_u64(my >> 5);
+        rel = (uint32_t)(my - w0 * 32);  // < 2^32: a group spans < 2^17 bits
+        const uint64_t lw = uniform_u64(last);
+        span = (lw >> 5) + 4 - w0;
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint32_t i = i0 + b * 64 + lane;
-            t[b] = E.words[min(w0 + i, E.n_words - 1)];  // unconditional (a load under a branch is waited at the join)
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const uint32_t i = i0 + b * 64 + lane;
-            if (i < nwin) win[i] = w0 + i < E.n_words ? __builtin_bswap32(t[b]) : 0u;
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    wave_lds_sync();
-    int32_t v[32];
-    parse_values<32>(E, win, nwin, w0, fits, my, v);
-    wave_lds_sync();
+        for (int b = 0; b < NWP; b++) t[b] = E.words[min(w0 + (uint64_t)(b * 64 + lane), E.n_words - 1)];
+    };
+    uint64_t w0, span;
+    uint32_t rel;
+    uint32_t pw[NWP];
     {
-        const uint32_t c = lane / PARTS, part = lane % PARTS;
-        char* cb = wl + c * G::SA_C;
+        uint64_t my, last;
+        __builtin_amdgcn_s_setprio(3);  // marks and window loads ahead of the computing waves
+        load_marks(lane0, cube_of(0), my, last);
+        open_window(lane0, my, last, w0, rel, span, pw);
+        __builtin_amdgcn_s_setprio(0);
+    }
+    for (int i = 0; i < NG; i++) {
+        const uint32_t cube0 = cube_of(i);
+        if (cube0 >= P.n_cubes) break;  // wave-uniform; every later group of the wave is past the end too
+        // the lane's addresses and constants are made inside each round, not hoisted and held across
+        // the transform (which needs the registers)
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_values)
+        const uint32_t nwin = (uint32_t)(fits ? span : 0);
 #pragma unroll
-        for (int i = 0; i < 32; i++) {
-            const uint32_t k = s_diag[part * 32 + i];
-            *(int32_t*)(cb + (k >> 6) * G::SA_F + (k & 63) * 4) = v[i];
+        for (int b = 0; b < NWP; b++) {
+            const uint32_t j = b * 64 + lane;
+            if (j < nwin) win[j] = w0 + j < E.n_words ? __builtin_bswap32(pw[b]) : 0u;
+        }
+        // the rest of a window longer than the look-ahead (content above 4 bits per value): 4 words per
+        // lane per round, all loads issued before the first LDS write
+        for (uint32_t i0 = NWP * 64; i0 < nwin; i0 += 256) {
+            uint32_t t[4];
+#pragma unroll
+            for (int b = 0; b < 4; b++) t[b] = E.words[min(w0 + i0 + b * 64 + lane, E.n_words - 1)];
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const uint32_t j = i0 + b * 64 + lane;
+                if (j < nwin) win[j] = w0 + j < E.n_words ? __builtin_bswap32(t[b]) : 0u;
+            }
+        }
+        uint64_t my_n = 0, last_n = 0;
+        if (i + 1 < NG) load_marks(lane, cube_of(i + 1), my_n, last_n);  // in flight during the parse
+        wave_lds_sync();
+        int32_t v[32];
+        parse_values<32>(E, win, nwin, w0, fits, w0 * 32 + rel, v);
+        if (i + 1 < NG) open_window(lane, my_n, last_n, w0, rel, span, pw);  // in flight during the transform
+        wave_lds_sync();
+        {
+            const uint32_t c = lane / PARTS, part = lane % PARTS;
+            char* cb = wl + c * G::SA_C;
+#pragma unroll
+            for (int j = 0; j < 32; j++) {
+                const uint32_t k = s_diag[part * 32 + j];
+                *(int32_t*)(cb + (k >> 6) * G::SA_F + (k & 63) * 4) = v[j];
+            }
+        }
+        wave_lds_sync();
+        decode_tile<D, 1, (NG > 1)>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, s_diag});
+        // the region receives the next group's window: after a block store (its rows are read by every
+        // wave of the block) the whole block must be past it (block-uniform condition, as dec_store_tile's)
+        if (i + 1 < NG) {
+            if (P.blk_store && cube0 - (uint32_t)wave * CPW + kWavesPerBlock * CPW <= P.n_cubes) __syncthreads();
+            else wave_lds_sync();
         }
     }
-    wave_lds_sync();
-    decode_tile<D, 1>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, s_diag});
 }
 
 // =============================================================================================
@@ -497,13 +546,29 @@ int launch_decode(int D, const DecodeParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, hipStream_t st) {
+namespace {
+template <int D, int NG>
+void launch_dec_eg_t(const DecodeParams& P, const EgDecParams& E, hipStream_t st) {
+    constexpr uint32_t cpw = DecGeom<D>::CPW;
+    const uint32_t groups = (P.n_cubes - P.cube_base + cpw - 1) / cpw;  // cube_base: a multiple of cpw
+    const uint32_t blocks = (groups + kWavesPerBlock * NG - 1) / (kWavesPerBlock * NG);
+    hipLaunchKernelGGL((decode_eg_kernel<D, NG>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+}
+template <int D>
+void launch_dec_eg_d(const DecodeParams& P, const EgDecParams& E, int ng, hipStream_t st) {
+    switch (ng) {
+        case 1: launch_dec_eg_t<D, 1>(P, E, st); break;
+        case 2: launch_dec_eg_t<D, 2>(P, E, st); break;
+        case 4: launch_dec_eg_t<D, 4>(P, E, st); break;
+        default: launch_dec_eg_t<D, 8>(P, E, st); break;
+    }
+}
+}  // namespace
+
+int launch_decode_eg(int D, const DecodeParams& P, const EgDecParams& E, int groups_per_wave, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
-    const uint32_t cpw = (D == 8) ? DecGeom<8>::CPW : DecGeom<4>::CPW;
-    const uint32_t waves = (P.n_cubes - P.cube_base + cpw - 1) / cpw;  // cube_base: a multiple of cpw
-    const uint32_t blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (D == 8) hipLaunchKernelGGL((decode_eg_kernel<8>), dim3(blocks), dim3(kBlock), 0, st, P, E);
-    else hipLaunchKernelGGL((decode_eg_kernel<4>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+    if (D == 8) launch_dec_eg_d<8>(P, E, groups_per_wave, st);
+    else launch_dec_eg_d<4>(P, E, groups_per_wave, st);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

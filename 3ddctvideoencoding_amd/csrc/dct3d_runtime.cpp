@@ -67,6 +67,7 @@ struct dct3d_ctx {
     bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
     bool opt_eg_force_retry = false;
+    int opt_eg_dec_groups = 0;  // fused stream decode: groups per wave (0: the default, 8)
     // certify-or-replay state
     uint64_t last_units = 0;
     bool last_valid = false;
@@ -294,6 +295,10 @@ int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_FORCE_RETRY: c->opt_eg_force_retry = value != 0.0; return DCT3D_OK;
+        case DCT3D_OPT_EG_DEC_GROUPS:
+            if (value != 0.0 && value != 1.0 && value != 2.0 && value != 4.0 && value != 8.0) return DCT3D_EINVAL;
+            c->opt_eg_dec_groups = (int)value;
+            return DCT3D_OK;
         default: return DCT3D_EINVAL;
     }
 }
@@ -1067,7 +1072,7 @@ static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int
     set_dec_replay(c, P);
     hipEvent_t* ev = timing_slot(c);
     if (ev) (void)hipEventRecord(ev[0], c->stream);
-    if (launch_decode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
+    if (launch_decode_eg(D, P, E, c->opt_eg_dec_groups ? c->opt_eg_dec_groups : 8, c->stream)) return DCT3D_EKERNEL;
     if (ev) {
         (void)hipEventRecord(ev[1], c->stream);
         (void)hipEventRecord(ev[2], c->stream);

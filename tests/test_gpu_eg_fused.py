@@ -279,3 +279,32 @@ def test_speculative_front_rerun_on_unresolved_pass0(pkg, oracle, plan8, gpu_ctx
     expect = plan8.decode_q(q, 128, 64, 24)
     for got in (ref_fused, ref_two, ref_host, got_fused, got_two, got_host):
         assert np.array_equal(got, expect)
+
+
+@pytest.mark.parametrize("groups", [1, 2, 4, 8])
+@pytest.mark.parametrize("depth", [8, 4])
+def test_fused_decode_groups_per_wave(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, groups):
+    """decode_eg_kernel runs `groups` rounds of 4 consecutive groups (2,048 values each) per block, the
+    next group's marks and window words in flight during the current one (DCT3D_OPT_EG_DEC_GROUPS; 0 =
+    8).  The same raster for every setting: 1080p uniform content (windows longer than the look-ahead
+    words), ragged frames (partial blocks: waves leaving the loop early, per-lane stores), dense long
+    codes (windows that do not fit the LDS: the global-memory parse)."""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    cases = [(1920, 1080, 2, "uniform"), (136, 72, 2, "ramp"), (24, 16, 3, "uniform")]
+    for w, h, stacks, kind in cases:
+        fr = pkg.synthetic.frames(w, h, stacks * depth, kind=kind, frame0=3)
+        data, tb = ctx.encode_eg(fr)
+        ref, reb = _decode_two_step(ctx, data, w, h, stacks)
+        with ctx_option(ctx, pkg.DCT3D_OPT_EG_DEC_GROUPS, groups):
+            got, eb = _decode_fused(ctx, data, w, h, stacks)
+        assert eb == reb == tb
+        assert np.array_equal(got, ref), (w, h, kind)
+    rng = np.random.default_rng(5 + depth)
+    n = ctx.n_cubes(64, 48, 2)
+    q = (rng.integers(2**24, 2**30, size=(n, depth, 8, 8)) * rng.choice([-1, 1], size=(n, depth, 8, 8))).astype(np.int32)
+    q[::2] = rng.integers(-9, 10, size=q[::2].shape)
+    data, nbits = _expected(oracle, pkg, q, depth)
+    with ctx_option(ctx, pkg.DCT3D_OPT_EG_DEC_GROUPS, groups):
+        got, eb = _decode_fused(ctx, data, 64, 48, 2)
+    assert eb == nbits
+    assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
