@@ -26,7 +26,7 @@ namespace dct3d {
 // monotone map x -> (byte) clamp(x, 0, 255) of InverseDCT.java:74-80 / Decoder.java:112, and equal
 // values at lo and hi prove the Java value (within [lo, hi]) maps to the same byte.
 // ---------------------------------------------------------------------------------------------
-constexpr int kDecWaveLds = 9216;
+constexpr int kDecWaveLds = 9280;  // 4 x (8 x 288 + 16) (8x8x8); 4 blocks per CU with the stream decode's s_diag
 
 template <int D>
 struct DecGeom {
@@ -34,7 +34,9 @@ struct DecGeom {
     static constexpr int LPC = 2 * D;          // lanes per cube
     static constexpr int CPW = 64 / LPC;       // cubes per wave: 4 (D=8) | 8 (D=4)
     static constexpr int SA_F = 288;           // staging face stride (256 B + 32 B pad)
-    static constexpr int SA_C = D * SA_F;      // staging cube stride
+    // staging cube stride; 8x8x8: + 16 B so that the wave's cubes start 4 banks apart (the layout-A reads of
+    // lanes (c1 = 0, 1) and the stream decode's value scatter over 4 cubes were 2- and 4-way bank conflicts)
+    static constexpr int SA_C = D * SA_F + (D == 8 ? 16 : 0);
     // B->C round strides (bank-conflict-free for D=8 by the guide's lane-group rules; D=4 best found)
     static constexpr int TZ = (D == 8) ? 528 : 256;    // z stride (D=8: 8 rows x 64 B + 16)
     static constexpr int TC = (D == 8) ? 2128 : 1040;  // cube stride

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     using G = DecGeom<D>;
     constexpr uint32_t CS = G::CS, PARTS = CS / 32, CPW = G::CPW;
     static_assert(CPW * CS == 2048 && PARTS * CPW == 64, "one wave = 64 marks");
-    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,304 words >= 2,048 values x 27 bits
+    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,320 words >= 2,048 values x 27 bits
     constexpr int NWP = 4;                     // window words per lane loaded ahead (256: 4 bits per value)
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];

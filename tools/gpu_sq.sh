@@ -13,5 +13,5 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
   timeout -k 10 240 rocprofv3 --pmc $grp -d $OUT/p$i -o p$i --output-format csv -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 $OUT/p$i.log; exit $rc; }
 done
-python3 tools/pmc_summary.py $OUT/summary.csv $(find $OUT -name "*counter_collection.csv")
+python3 tools/pmc_summary.py $OUT/summary.csv $OUT
 grep -v "synth" $OUT/summary.csv
