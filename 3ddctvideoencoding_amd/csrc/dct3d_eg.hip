@@ -461,10 +461,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
         // pass), then the checked steps; an invalid code leaves the lean loop unconsumed.
         const uint32_t fast_stop = stop > 128u ? stop - 128u : 0u;
         while (r.pos < fast_stop) {
-            n += r.ones(64u);
+            n += r.ones<true>(64u);
             if (!r.at_long_code()) continue;  // refill
             uint32_t code;
-            if (!r.get(code)) break;
+            if (!r.get<true>(code)) break;
             n++;
         }
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
@@ -567,13 +567,15 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
     while (r.pos < fast_end && i < fast_rem) {
         const uint32_t p0 = r.pos;
-        const uint32_t k = r.ones(64u);
-        for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
-            mk[(ph + j) / kMarkVals] = base + p0 + (j - i);
+        const uint32_t k = r.ones<true>(64u);
+        // the run's marks: values i + d0 and i + d0 + 32 (a run of <= 64 holds at most two)
+        const uint32_t d0 = (kMarkVals - ((ph + i) & (kMarkVals - 1))) & (kMarkVals - 1);
+        if (d0 < k) mk[(ph + i + d0) / kMarkVals] = base + p0 + d0;
+        if (d0 + kMarkVals < k) mk[(ph + i + d0) / kMarkVals + 1] = base + p0 + d0 + kMarkVals;
         i += k;
         if (!r.at_long_code()) continue;  // refill
         const uint32_t p1 = r.pos;
-        if (!r.get(code)) break;  // invalid: nothing consumed, the checked loop reports it
+        if (!r.get<true>(code)) break;  // invalid: nothing consumed, the checked loop reports it
         if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p1;
         i++;
     }
