@@ -400,6 +400,10 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     constexpr int NWP = 4;                     // window words per lane loaded ahead (256: 4 bits per value)
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];
+    // staging byte offset (within a cube) of stream position part * 32 + j at s_soff[part * SOFF + j]:
+    // rows of 40 entries (80 B), so that the 16 parts' 16-byte reads fall on distinct banks
+    constexpr uint32_t SOFF = 40;
+    __shared__ __attribute__((aligned(16))) uint16_t s_soff[PARTS * SOFF];
     dec_clear_next_slot(P);
     // corrupt / short / empty stream: reported by the mark pass (block-uniform)
     if (E.status[2] != 0 || E.n_words == 0) return;
@@ -409,7 +413,11 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
 #pragma unroll
         for (uint32_t r = 0; r < CS / kBlock; r++) t[r] = E.diag[threadIdx.x + r * kBlock];
 #pragma unroll
-        for (uint32_t r = 0; r < CS / kBlock; r++) s_diag[threadIdx.x + r * kBlock] = t[r];
+        for (uint32_t r = 0; r < CS / kBlock; r++) {
+            const uint32_t i = threadIdx.x + r * kBlock, k = t[r];
+            s_diag[i] = t[r];
+            s_soff[(i / 32) * SOFF + i % 32] = (uint16_t)((k >> 6) * G::SA_F + (k & 63) * 4);
+        }
     }
     __syncthreads();
     const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -478,13 +486,17 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         parse_values<32>(E, win, nwin, w0, fits, w0 * 32 + rel, v);
         if (i + 1 < NG) open_window(lane, my_n, last_n, w0, rel, span, pw);  // in flight during the transform
         wave_lds_sync();
-        {
+        {  // each value to its diagonal position in the staging: 8 offsets per 16-byte table read
             const uint32_t c = lane / PARTS, part = lane % PARTS;
             char* cb = wl + c * G::SA_C;
+            const uint4* so = (const uint4*)(s_soff + part * SOFF);
 #pragma unroll
-            for (int j = 0; j < 32; j++) {
-                const uint32_t k = s_diag[part * 32 + j];
-                *(int32_t*)(cb + (k >> 6) * G::SA_F + (k & 63) * 4) = v[j];
+            for (int q = 0; q < 4; q++) {
+                const uint4 o = so[q];
+                const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    *(int32_t*)(cb + ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu)) = v[q * 8 + e];
             }
         }
         wave_lds_sync();
