@@ -188,7 +188,8 @@ struct WinReader {
 // position after a wave-uniform test.
 struct ValidWinReader {
     const uint32_t* s;
-    uint32_t next;   // index of the word held in `pre`; the buffer ends at bit next * 32
+    const uint32_t* np;  // the word held in `pre` (a pointer, not an index: one add per refill, no address
+                         // arithmetic); the buffer ends at bit (np - s) * 32
     uint32_t hi, lo;
     uint32_t avail;
     uint32_t pre;
@@ -198,15 +199,15 @@ struct ValidWinReader {
         hi = (uint32_t)(b >> 32);
         lo = (uint32_t)b;
         avail = 64u - (p & 31);
-        next = k + 2;
-        pre = s[next];
+        np = s + k + 2;
+        pre = *np;
     }
     __device__ __forceinline__ uint32_t get() {
         if (avail < 32u) {  // hi holds the avail valid bits, lo is zero: pre goes right behind them
             hi |= pre >> avail;
             lo = __builtin_amdgcn_alignbit(pre, 0u, avail);  // pre << (32 - avail); 0 for avail = 0
             avail += 32u;
-            pre = s[++next];
+            pre = *++np;
         }
         const uint32_t z = __builtin_clz(hi);  // a valid code: hi (>= 32 buffered bits) is not 0
         const uint32_t w = 2u * z + 1u;
@@ -216,7 +217,7 @@ struct ValidWinReader {
         avail -= w;
         if (__builtin_expect(__ballot(z >= 16u) != 0ull, 0)) {
             if (z >= 16u) {  // a code of 33+ bits: read at its absolute position
-                const uint32_t p = next * 32u - (avail + w);
+                const uint32_t p = (uint32_t)(np - s) * 32u - (avail + w);
                 const uint32_t k = p >> 5;
                 const int sh = (int)(p & 31);
                 const uint64_t h = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
@@ -252,7 +253,7 @@ template <int N>
 __device__ __forceinline__ void parse_values(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
                                              bool fits, uint64_t my, int32_t (&v)[N]) {
     if (fits) {
-        ValidWinReader r{win, 0, 0, 0, 0, 0};
+        ValidWinReader r{win, nullptr, 0, 0, 0, 0};
         r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
 #pragma unroll
         for (int i = 0; i < N; i++) v[i] = eg_value_fast(r.get());
