@@ -436,8 +436,10 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     // words up to the end mark (+4 slack); its first NWP * 64 words requested (clamped into the stream)
     auto open_window = [&](int lane, uint64_t my, uint64_t last, uint64_t& w0, uint32_t& rel, uint64_t& span,
                            uint32_t (&t)[NWP]) {
-        w0 = uniform_u64(my >> 5);
-        rel = (uint32_t)(my - w0 * 32);  // < 2^32: a group spans < 2^17 bits
+        w0 = uniform_u64(my >> 5);  // lane 0's mark: lane 0 of a live group is always a real mark
+        // < 2^17 for a real mark (a group spans < 2^17 bits); a lane past the last mark (my = 0: the
+        // unused cubes of a partial last group) parses from the window's first bit, inside the window
+        rel = my > w0 * 32 ? (uint32_t)(my - w0 * 32) : 0u;
         const uint64_t lw = uniform_u64(last);
         span = (lw >> 5) + 4 - w0;
 #pragma unroll

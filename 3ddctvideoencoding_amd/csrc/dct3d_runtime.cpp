@@ -271,9 +271,16 @@ int dct3d_ctx_set_stream(dct3d_ctx* c, void* s) {
         // work enqueued on the new stream runs after the old stream's: a later launch would otherwise
         // overlap an earlier one whose block 0 clears the counter slot the later one counts into
         if (hipSetDevice(c->device) != hipSuccess) return DCT3D_EDEVICE;
-        if ((!c->ev_switch && hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess) ||
-            hipEventRecord(c->ev_switch, c->stream) != hipSuccess || hipStreamWaitEvent(ns, c->ev_switch, 0) != hipSuccess)
+        if (!c->ev_switch && hipEventCreateWithFlags(&c->ev_switch, hipEventDisableTiming) != hipSuccess)
             return DCT3D_EDEVICE;
+        if (hipEventRecord(c->ev_switch, c->stream) == hipSuccess) {
+            if (hipStreamWaitEvent(ns, c->ev_switch, 0) != hipSuccess) return DCT3D_EDEVICE;
+        } else {
+            // the old stream is gone (a caller's short-lived stream destroyed before the switch): its
+            // work was still ordered by a device-wide synchronisation, which covers it either way
+            (void)hipGetLastError();
+            if (hipDeviceSynchronize() != hipSuccess) return DCT3D_EDEVICE;
+        }
     }
     c->stream = ns;
     return DCT3D_OK;

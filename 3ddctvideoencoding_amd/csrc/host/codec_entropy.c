@@ -151,11 +151,9 @@ static int pz_drain(dct3d_entropy_enc *e, int wait) {
 
 static int pz_submit(dct3d_entropy_enc *e, int last) {
     pz_state *p = e->pz;
-    if (!p->started) {
-        for (int t = 0; t < p->threads; t++)
-            if (pthread_create(&p->tid[t], NULL, pz_worker, p)) return -1;
-        p->started = p->threads;
-    }
+    /* counted one by one, so that pz_destroy wakes and joins exactly the workers that exist */
+    for (; p->started < p->threads; p->started++)
+        if (pthread_create(&p->tid[p->started], NULL, pz_worker, p)) return -1;
     if (!p->header_done) {  /* zlib header: deflate, 32 KiB window, FLEVEL 3 (level 9) */
         static const unsigned char hdr[2] = {0x78, 0xDA};
         if (sink(e, hdr, 2)) return -1;

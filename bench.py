@@ -34,6 +34,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CONFIGS = {
     # name: (width, height, block_depth, stacks per GPU, direction); stacks None = a fixed job split
     # over the ranks (JOB_STACKS, strong scaling)
+    # BASELINE config 1: the reference's own CPU-runnable case, the Java Encoder path (Encoder.java:47-89)
+    # on one 64x64 8-frame stack, no GPU: timed through its restatement (bench_c1, n_gpus 0)
+    "c1_java_cpu_64x64": (64, 64, 8, 1, "java_cpu"),
     "c2_encode_1080p": (1920, 1080, 8, 128, "encode"),
     "c3_decode_1080p": (1920, 1080, 8, 128, "decode"),
     # BASELINE config 4: ONE job of 64 4K stacks, each rank encodes shard(64, N, rank) of them
@@ -53,6 +56,7 @@ CONFIGS = {
 
 # what one step computes, per direction (the headline metric is BASELINE.json's, config c2)
 WHAT = {
+    "java_cpu": "forward 3D DCT + quantise, the Java CPU Encoder path (restated), no GPU",
     "encode": "forward 3D DCT + quantise",
     "decode": "dequantise + inverse 3D DCT",
     "encode_eg": "forward 3D DCT + quantise + diagonal order + Exp-Golomb stream",
@@ -71,7 +75,8 @@ def metric_name(direction: str, depth: int, width: int = 1920, height: int = 108
         return HEADLINE_METRIC
     unit = "8×8×8" if depth == 8 else "8×8×4"
     size = "1080p" if (width, height) == (1920, 1080) else f"{width}×{height}"
-    return f"{unit} cubes/s ({WHAT[direction]}) on {size}×{depth}-frame stacks; % HBM roofline"
+    tail = "" if direction == "java_cpu" else "; % HBM roofline"
+    return f"{unit} cubes/s ({WHAT[direction]}) on {size}×{depth}-frame stacks{tail}"
 
 
 def parse():
@@ -176,6 +181,76 @@ def cpu_baseline(width, height, depth, budget_s, kind):
             "kind": "port",
             "sample": f"{stacks} x {width}x{height}x{depth} stack(s) ({done} cubes) through the restated Java "
                       f"DCT.run + Encoder quantisation, {threads} threads, {t_total:.1f} s"}
+
+
+def bench_c1(a):
+    """BASELINE config 1: the Java CPU Encoder path on one 64x64 8-frame stack (Encoder.java:47-89: the
+    DCT's Transform.run over a fixed pool of availableProcessors() threads, one task per cube,
+    Transform.java:63-104, then the Math.round quantisation into cube-major order).  The JVM cannot run
+    here (no JDK); the restatement (oracle/java_dct3d.c, the same grouping, memoisation and pool) is
+    what is timed, so `kind` is "port".  A step = one encode of the stack (DCT.run + quantisation); the
+    per-file DCT setup (DCT.initialize + createSums, DCT.java:77-163) is timed once beside it.  No GPU:
+    n_gpus 0, no roofline.  The output digest lets a test compare the step's result with the committed
+    golden fixture (tests/golden/c1_64x64x8.npz)."""
+    import hashlib
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test infrastructure: config 1 IS the CPU reference path, timed as its restatement
+
+    width, height, depth = CONFIGS[a.config][:3]
+    syn = importlib.import_module("3ddctvideoencoding_amd.synthetic")
+    avail, avail_src = java_available_processors()
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(avail, env) if env > 0 else avail
+    fr = syn.frames(width, height, depth, kind=a.kind)
+    t0 = time.perf_counter()
+    plan = oracle.Plan(8, 8, depth)
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(a.warmup):
+        plan.encode_q(fr, threads=threads)
+    # repeats: a step is ~1 ms of work, so every step is timed on its own and the line takes the mean
+    times, q = [], None
+    t_all = time.perf_counter()
+    for _ in range(a.steps):
+        t0 = time.perf_counter()
+        q = plan.encode_q(fr, threads=threads)
+        times.append(time.perf_counter() - t0)
+    elapsed = time.perf_counter() - t_all
+    cubes = (width // 8) * (height // 8)  # one stack
+    ms = sorted(1e3 * t for t in times)
+    value = cubes * a.steps / sum(times)
+    base = {"value": value, "unit": "cubes/s", "cores": threads, "threads": threads,
+            "host_cores": os.cpu_count(), "available_processors": avail,
+            "pool_rule": f"availableProcessors() = {avail} ({avail_src})"
+                         + (f", capped by OMP_NUM_THREADS={env} (this box's CPU share)" if 0 < env < avail else ""),
+            "kind": "port",
+            "sample": f"{a.steps} encodes of one {width}x{height}x{depth} stack ({cubes} cubes each) through the "
+                      f"restated Java DCT.run + Encoder quantisation, {threads} threads, {sum(times):.3f} s"}
+    res = {
+        "metric": metric_name("java_cpu", depth, width, height),
+        "value": value,
+        "unit": "cubes/s",
+        "n_gpus": 0,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * sum(times) / a.steps,
+        "ms_per_step_median": ms[len(ms) // 2],
+        "ms_per_step_min": ms[0],
+        "wall_s": elapsed,
+        "higher_is_better": True,
+        "scaling": None,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "dtype_note": "the Java path's fp64 grouped fold (DCT.java:41-59, Sum.java:41-52), Math.round",
+        "data": "synthetic",
+        "config": {"workload": f"{width}x{height} grayscale, one {depth}-frame stack, {WHAT['java_cpu']}",
+                   "name": a.config, "content": a.kind, "cubes_per_step": cubes, "parallelism": f"{threads} threads"},
+        "plan_ms": plan_ms,
+        "roofline": None,
+        "output_sha256": hashlib.sha256(q.tobytes()).hexdigest(),
+        "cpu_baseline": base,
+    }
+    print(json.dumps(res), flush=True)
 
 
 def pmc_traffic(config: str, kernel: str, depth: int):
@@ -314,6 +389,10 @@ def xgmi_leg(ctx, torch, dist, sharding, frames, q, n_all, depth, width, height,
 def main():
     a = parse()
     width, height, depth, stacks, direction = CONFIGS[a.config]
+    if direction == "java_cpu":
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            raise SystemExit("c1_java_cpu_64x64 is the CPU reference path: run it without torch.distributed")
+        return bench_c1(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

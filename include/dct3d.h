@@ -114,7 +114,9 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
 void dct3d_ctx_destroy(dct3d_ctx *ctx);
 
 /* Use an external hipStream_t (e.g. a framework's current stream) instead of the ctx-owned one.
- * NULL restores the ctx-owned stream. */
+ * NULL restores the ctx-owned stream.  Work enqueued afterwards is ordered after the previous
+ * stream's work (an event on it; should that stream already be destroyed, a device-wide
+ * synchronisation instead). */
 int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
 /* The ctx's device ordinal, block depth and the hipStream_t its calls run on (any pointer may be
  * NULL).  Lets companion libraries (libdct3d_diag.so) queue work in order with the ctx's. */

@@ -46,11 +46,14 @@ def main():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), frames=fr, q=q, dct=d, decoded=dec, eg=eg)
         print(name, q.shape, "eg bytes", eg.size)
     dig = {}
-    for key, plan, w, h, f, kind in (("1080p_ramp_q", p8, 1920, 1080, 8, "ramp"),
-                                     ("1080p_uniform_q", p8, 1920, 1080, 8, "uniform"),
-                                     ("4k_ramp_q", p8, 3840, 2160, 8, "ramp"),
-                                     ("1080p_d4_ramp_q", p4, 1920, 1080, 4, "ramp")):
-        q = plan.encode_q(syn.frames(w, h, f, kind=kind))
+    # frame0: the stack's first frame in the synthetic video; 4k_stack63 is the last stack of config 4's
+    # 64-stack job (frames 504..511), as bench.py --config c4_encode_4k encodes it at N = 1
+    for key, plan, w, h, f, kind, f0 in (("1080p_ramp_q", p8, 1920, 1080, 8, "ramp", 0),
+                                         ("1080p_uniform_q", p8, 1920, 1080, 8, "uniform", 0),
+                                         ("4k_ramp_q", p8, 3840, 2160, 8, "ramp", 0),
+                                         ("1080p_d4_ramp_q", p4, 1920, 1080, 4, "ramp", 0),
+                                         ("4k_stack63_ramp_q", p8, 3840, 2160, 8, "ramp", 63 * 8)):
+        q = plan.encode_q(syn.frames(w, h, f, kind=kind, frame0=f0))
         dig[key] = hashlib.sha256(q.tobytes()).hexdigest()
         print(key, dig[key])
     with open(os.path.join(HERE, "digests.json"), "w") as fh:
