@@ -190,7 +190,44 @@ typedef struct {
     int treeified;
 } jplan;
 
-static double java_coef(const jplan *p, double scale, int k0, int k1, int k2, int n0, int n1, int n2) {
+/* Residual study only (tools/cos_ulp_sensitivity.py, tests/test_cos_residual.py): an alternative
+ * plan whose Math.cos differs from glibc's correctly rounded cos at chosen arguments by +-1 ulp, and/or
+ * whose exactly rational coefficients (c * 1E9 within 1e-6 of an integer K, DCT.java:112-116) take the
+ * other integer key.  key_flip: 0 none, 1 toggle (K <-> K - sign), 2 all to K - sign, 3 all to K.
+ * The default plan (oracle_plan_create) uses none of this. */
+typedef struct {
+    const double *args;
+    const int8_t *delta;
+    int n;
+    int key_flip;
+} cosalt;
+
+static double java_cos(double a, const cosalt *alt) {
+    double c = cos(a);
+    if (alt)
+        for (int i = 0; i < alt->n; i++)
+            if (alt->args[i] == a && alt->delta[i]) {
+                c = nextafter(c, alt->delta[i] > 0 ? INFINITY : -INFINITY);
+                break;
+            }
+    return c;
+}
+
+static int64_t java_key(double coef, const cosalt *alt) {
+    int64_t key = java_d2l(coef * 1E9);
+    if (!alt || !alt->key_flip) return key;
+    const double x = coef * 1E9, K = nearbyint(x);
+    if (fabs(x - K) >= 1e-6 || K == 0.0) return key;   /* not a rational coefficient's key */
+    const int64_t ki = (int64_t)K, lo = ki - (x > 0 ? 1 : -1); /* the two candidate keys */
+    switch (alt->key_flip) {
+    case 1: return key == ki ? lo : ki;
+    case 2: return lo;
+    default: return ki;
+    }
+}
+
+static double java_coef_alt(const jplan *p, double scale, int k0, int k1, int k2, int n0, int n1, int n2,
+                            const cosalt *alt) {
     /* Transform.java:20-21 */
     const double INVERSE_SQRT_2 = 1.0 / sqrt(2.0);
     /* DCT.java:81-84: Math.PI / (float) N -> double */
@@ -207,9 +244,9 @@ static double java_coef(const jplan *p, double scale, int k0, int k1, int k2, in
     double c = scale * c0;
     c = c * c1;
     c = c * c2;
-    c = c * cos(a0);
-    c = c * cos(a1);
-    c = c * cos(a2);
+    c = c * java_cos(a0, alt);
+    c = c * java_cos(a1, alt);
+    c = c * java_cos(a2, alt);
     return c;
 }
 
@@ -232,7 +269,7 @@ static int cmp_int(const void *a, const void *b) {
     return (x > y) - (x < y);
 }
 
-jplan *oracle_plan_create(int cw, int ch, int cd) {
+static jplan *plan_create(int cw, int ch, int cd, const cosalt *alt) {
     jplan *p = (jplan *)calloc(1, sizeof(jplan));
     p->cw = cw; p->ch = ch; p->cd = cd;
     int cs = cw * ch * cd;
@@ -274,8 +311,8 @@ jplan *oracle_plan_create(int cw, int ch, int cd) {
                 for (int n0 = 0; n0 < cd; n0++)
                     for (int n1 = 0; n1 < ch; n1++)
                         for (int n2 = 0; n2 < cw; n2++) {
-                            double coef = java_coef(p, scale, k0, k1, k2, n0, n1, n2);
-                            int64_t key = java_d2l(coef * 1E9);
+                            double coef = java_coef_alt(p, scale, k0, k1, k2, n0, n1, n2, alt);
+                            int64_t key = java_key(coef, alt);
                             if (key == 0) continue; /* DCT.java:84 */
                             int g = jmap_get(&m, key);
                             if (g < 0) {
@@ -346,11 +383,19 @@ jplan *oracle_plan_create(int cw, int ch, int cd) {
                     for (int k1 = 0; k1 < ch; k1++)
                         for (int k2 = 0; k2 < cw; k2++) {
                             int ik = (k0 * ch + k1) * cw + k2;
-                            p->inv_coef[(size_t)on * cs + ik] = java_coef(p, scale, k0, k1, k2, n0, n1, n2);
+                            p->inv_coef[(size_t)on * cs + ik] = java_coef_alt(p, scale, k0, k1, k2, n0, n1, n2, alt);
                         }
             }
     free(gcount); free(gmem); free(gfirst_coef_idx); free(gcoef); free(slots); free(tmp);
     return p;
+}
+
+jplan *oracle_plan_create(int cw, int ch, int cd) { return plan_create(cw, ch, cd, NULL); }
+
+/* the residual study's alternative plan (cosalt above): n (argument, +-1 ulp) pairs, key_flip mode */
+jplan *oracle_plan_create_alt(int cw, int ch, int cd, const double *args, const int8_t *delta, int n, int key_flip) {
+    const cosalt alt = {args, delta, n, key_flip};
+    return plan_create(cw, ch, cd, &alt);
 }
 
 void oracle_plan_destroy(jplan *p) {

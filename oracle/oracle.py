@@ -38,6 +38,8 @@ def lib() -> C.CDLL:
         vp, i32, f64 = C.c_void_p, C.c_int, C.c_double
         L.oracle_plan_create.restype = vp
         L.oracle_plan_create.argtypes = [i32, i32, i32]
+        L.oracle_plan_create_alt.restype = vp
+        L.oracle_plan_create_alt.argtypes = [i32, i32, i32, vp, vp, i32, i32]
         L.oracle_plan_destroy.argtypes = [vp]
         for name in ("oracle_plan_n_mults", "oracle_plan_n_sums", "oracle_plan_treeified"):
             getattr(L, name).restype = i32
@@ -80,10 +82,20 @@ def default_threads() -> int:
 class Plan:
     """DCT.initialize/createSums + InverseDCT.initialize for one cube shape (cw, ch, cd)."""
 
-    def __init__(self, cw: int = 8, ch: int = 8, cd: int = 8):
+    def __init__(self, cw: int = 8, ch: int = 8, cd: int = 8, cos_ulp=None, key_flip: int = 0):
+        """cos_ulp / key_flip: the Math.cos residual study only (tools/cos_ulp_sensitivity.py) -- an
+        alternative plan whose Math.cos is 1 ulp off glibc's at the given arguments ({arg: +-1}), and/or
+        whose exactly rational coefficients take the other integer key (java_dct3d.c, cosalt)."""
         self.cw, self.ch, self.cd = cw, ch, cd
         self.cs = cw * ch * cd
-        self._p = lib().oracle_plan_create(cw, ch, cd)
+        if cos_ulp is None and not key_flip:
+            self._p = lib().oracle_plan_create(cw, ch, cd)
+        else:
+            items = sorted((cos_ulp or {}).items())
+            self._args = np.array([a for a, _ in items] or [0.0], np.float64)
+            self._delta = np.array([d for _, d in items] or [0], np.int8)
+            self._p = lib().oracle_plan_create_alt(cw, ch, cd, _ptr(self._args), _ptr(self._delta), len(items),
+                                                   int(key_flip))
 
     def __del__(self):
         try:

@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""The Math.cos residual, counted (VERDICT r3 "next" #2).  TEST / STUDY INFRASTRUCTURE (uses oracle/).
+
+The Java plan (DCT.initialize, DCT.java:104-131; InverseDCT.initialize, InverseDCT.java:110-124) is a
+function of Math.cos at a few dozen arguments.  The oracle and the product planner use glibc cos, which is
+correctly rounded at every one of them (tests/test_plan.py); Java only promises 1 ulp.  Every group key
+(long)(c * 1E9) is stable under a 1-ulp cosine except those of the exactly rational coefficients (+-1/32,
++-1/16: 24 outputs at 8^3, 39 at 8x8x4), whose keys -- and hence groups and HashMap fold order -- follow
+the cosine's last bit.  This study builds the alternative plans such a JVM could have and counts how many
+quantised outputs (encode) and decoded bytes (decode) of the committed corpora change under each:
+
+  key_flip 1/2/3   the rational coefficients' keys toggled / all on the K - 1 side / all on the K side
+                   (the "adjacent integer" plans: what a cosine 1 ulp off at their arguments yields)
+  cos +-1 ulp      Math.cos 1 ulp above / below glibc at ONE argument (every nonzero argument, both ways)
+  random           Math.cos in {-1, 0, +1} ulp at every argument independently (seeded)
+
+An output can change only where Java's fp64 value stands within the plans' difference of a rounding
+boundary: q = v / step within TAU of x.5 (Math.round, Encoder.java:75-89) or a decoded pixel within TAU of
+an integer ((byte) truncation, Decoder.java:107-117).  The plans differ by a few ulps per coefficient and
+by the fold order, |dv| < 1e-9 (checked: `max_dv` below), so TAU = 1e-6 leaves > 1000x margin.  Only the
+cubes holding such a candidate are re-run under each alternative (the full corpora are re-run for every
+alternative on the 64x64 fixtures, tests/test_cos_residual.py, to check the filter).
+
+    python tools/cos_ulp_sensitivity.py [--quick] [--out profiles/r04/cos_residual.json]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle  # noqa: E402
+
+syn = importlib.import_module("3ddctvideoencoding_amd.synthetic")
+
+TAU = 1e-6
+
+
+def cos_args(n: int) -> list[float]:
+    """The nonzero arguments DCT.initialize passes to Math.cos on an axis of length n: (Math.PI /
+    (float) n) * (m + 0.5f) * k, left to right (DCT.java:104-112).  k = 0 gives cos(0) = 1."""
+    f32 = lambda v: float(np.float32(v))
+    p = math.pi / f32(n)
+    return sorted({p * f32(m + 0.5) * k for m in range(n) for k in range(1, n)})
+
+
+def alternatives(depth: int, n_random: int = 24, seed: int = 4):
+    """[(name, Plan kwargs)] of the alternative plans."""
+    args = sorted(set(cos_args(8)) | (set(cos_args(4)) if depth == 4 else set()))
+    alts = [(f"key_flip{m}", {"key_flip": m}) for m in (1, 2, 3)]
+    for i, a in enumerate(args):
+        for d in (1, -1):
+            alts.append((f"cos[{i}]{'+' if d > 0 else '-'}1ulp", {"cos_ulp": {a: d}}))
+    rng = np.random.default_rng(seed)
+    for r in range(n_random):
+        alts.append((f"random{r}", {"cos_ulp": {a: int(d) for a, d in zip(args, rng.integers(-1, 2, len(args)))}}))
+    return alts
+
+
+def corpora(depth: int, quick: bool = False):
+    """(name, frames u8 [F, H, W]) -- the committed golden fixtures' inputs and the digest stacks."""
+    out = [("64x64 ramp", syn.frames(64, 64, depth, kind="ramp")),
+           ("64x64 uniform", syn.frames(64, 64, depth, kind="uniform"))]
+    if quick:
+        return out
+    out += [("1080p ramp", syn.frames(1920, 1080, depth, kind="ramp")),
+            ("1080p uniform", syn.frames(1920, 1080, depth, kind="uniform")),
+            ("4K ramp", syn.frames(3840, 2160, depth, kind="ramp"))]
+    if depth == 8:
+        out.append(("4K ramp stack 63", syn.frames(3840, 2160, 8, kind="ramp", frame0=504)))
+    return out
+
+
+def _steps(depth):
+    s = np.arange(depth)[:, None, None] + np.arange(8)[None, :, None] + np.arange(8)[None, None, :]
+    return np.maximum(1, 5 * s).astype(np.float64)
+
+
+def _mini(cubes, depth):
+    """cube-major [m, cd, 8, 8] -> a raster [cd, 8, 8 m] holding them side by side."""
+    m = cubes.shape[0]
+    return oracle.from_cubes(np.ascontiguousarray(cubes), 8 * m, 8, depth)
+
+
+class Corpus:
+    """Base (glibc-cos) encode and decode of one corpus, and its rounding-boundary candidates."""
+
+    def __init__(self, name, fr, base: oracle.Plan):
+        self.name, self.depth = name, base.cd
+        F, H, W = fr.shape
+        H8, W8 = H - H % 8, W - W % 8
+        fr = np.ascontiguousarray(fr[:, :H8, :W8])
+        self.q, d = base.encode_q(fr, want_dct=True)
+        v = oracle.to_cubes(d, cd=self.depth)
+        t = v / _steps(self.depth)                      # Java: dct / quant in fp64 (Encoder.java:85)
+        self.enc_dist = np.abs(t - np.floor(t) - 0.5)
+        self.enc_cand = np.nonzero((self.enc_dist < TAU).reshape(len(v), -1).any(1))[0]
+        self.cubes_u8 = oracle.to_cubes(fr, cd=self.depth)
+        self.n_enc = self.q.size
+        # decode of the encoder's output (Decoder.java:78-117): pre-truncation pixels
+        deq = oracle.dequantize(self.q, W8, H8, F, cd=self.depth)
+        px = base.idct(deq)
+        pc = oracle.to_cubes(px, cd=self.depth)
+        self.dec_dist = np.abs(pc - np.rint(pc))
+        self.dec_cand = np.nonzero((self.dec_dist < TAU).reshape(len(pc), -1).any(1))[0]
+        self.deq_cubes = oracle.to_cubes(deq, cd=self.depth)
+        self.dec_base = np.trunc(pc)
+        self.px_base = pc
+        self.n_dec = pc.size
+
+    def run(self, alt: oracle.Plan, full: bool = False):
+        """(changed quantised outputs, changed decoded bytes, max |dv| seen) under plan `alt`.  full:
+        every cube, and assert that every change lies at a candidate (the filter is sound)."""
+        D = self.depth
+        ce = np.arange(len(self.cubes_u8)) if full else self.enc_cand
+        de = np.arange(len(self.deq_cubes)) if full else self.dec_cand
+        n_e = n_d = 0
+        max_dv = 0.0
+        if len(ce):
+            qa, da = alt.encode_q(_mini(self.cubes_u8[ce], D), want_dct=True)
+            qa = qa.reshape(len(ce), D, 8, 8)
+            diff = qa != self.q.reshape(-1, D, 8, 8)[ce]
+            if full:
+                assert (self.enc_dist[ce][diff] < TAU).all(), self.name
+            n_e = int(diff.sum())
+        if len(de):
+            pa = oracle.to_cubes(alt.idct(_mini(self.deq_cubes[de], D)), cd=D)
+            diff = np.trunc(pa) != self.dec_base[de]
+            max_dv = float(np.abs(pa - self.px_base[de]).max())
+            if full:
+                assert (self.dec_dist[de][diff] < TAU).all(), self.name
+            n_d = int(diff.sum())
+        return n_e, n_d, max_dv
+
+
+def enc_value_spread(corp: Corpus, alt: oracle.Plan, base: oracle.Plan) -> float:
+    """max |v_alt - v_base| of the forward DCT values over the corpus (Java fp64 values, all cubes)."""
+    D = corp.depth
+    mini = _mini(corp.cubes_u8, D)
+    _, da = alt.encode_q(mini, want_dct=True)
+    _, db = base.encode_q(mini, want_dct=True)
+    return float(np.abs(da - db).max())
+
+
+def study(depth: int, quick: bool = False, n_random: int = 24, log=print):
+    base = oracle.Plan(8, 8, depth)
+    corp = []
+    for name, fr in corpora(depth, quick):
+        t0 = time.time()
+        corp.append(Corpus(name, fr, base))
+        c = corp[-1]
+        log(f"  [{depth}] {name}: {c.n_enc} coefficients, {len(c.enc_cand)} encode-candidate cubes "
+            f"(min dist {c.enc_dist.min():.3g}), {len(c.dec_cand)} decode-candidate cubes "
+            f"(min dist {c.dec_dist.min():.3g})  {time.time() - t0:.1f}s")
+    alts = alternatives(depth, n_random)
+    res = {"depth": depth, "tau": TAU, "n_alternatives": len(alts), "corpora": {}}
+    per = {c.name: {"coefficients": c.n_enc, "pixels": c.n_dec, "encode_candidate_cubes": len(c.enc_cand),
+                    "encode_candidates": [int(x) for x in c.enc_cand],
+                    "decode_candidate_cubes": len(c.dec_cand), "encode_min_dist": float(c.enc_dist.min()),
+                    "decode_min_dist": float(c.dec_dist.min()), "changed": {}} for c in corp}
+    max_dv = 0.0
+    spread = 0.0
+    for an, kw in alts:
+        alt = oracle.Plan(8, 8, depth, **kw)
+        for c in corp:
+            ne, nd, dv = c.run(alt)
+            max_dv = max(max_dv, dv)
+            if ne or nd:
+                per[c.name]["changed"][an] = [ne, nd]
+        spread = max(spread, enc_value_spread(corp[0], alt, base))
+    for c in corp:
+        ch = per[c.name]["changed"]
+        per[c.name]["max_changed_encode"] = max([v[0] for v in ch.values()], default=0)
+        per[c.name]["max_changed_decode"] = max([v[1] for v in ch.values()], default=0)
+        per[c.name]["alternatives_changing"] = len(ch)
+    tot_e = sum(c.n_enc for c in corp)
+    tot_d = sum(c.n_dec for c in corp)
+    worst_e = max(sum(per[c.name]["changed"].get(an, [0, 0])[0] for c in corp) for an, _ in alts)
+    worst_d = max(sum(per[c.name]["changed"].get(an, [0, 0])[1] for c in corp) for an, _ in alts)
+    res.update(corpora=per, total_coefficients=tot_e, total_pixels=tot_d,
+               worst_alternative_changed_encode=worst_e, worst_alternative_changed_decode=worst_d,
+               encode_per_1e8=worst_e / tot_e * 1e8, decode_per_1e8=worst_d / tot_d * 1e8,
+               max_decode_dv=max_dv, max_encode_dv_64x64=spread)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true", help="64x64 corpora only")
+    ap.add_argument("--random", type=int, default=24)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    out = {}
+    for depth in (8, 4):
+        t0 = time.time()
+        r = study(depth, a.quick, a.random)
+        r["seconds"] = round(time.time() - t0, 1)
+        out[f"depth{depth}"] = r
+        print(json.dumps({k: v for k, v in r.items() if k != "corpora"}))
+        for name, c in r["corpora"].items():
+            print(f"    {name}: max changed encode {c['max_changed_encode']} decode {c['max_changed_decode']} "
+                  f"({c['alternatives_changing']} of {r['n_alternatives']} alternatives change something)")
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
