@@ -373,28 +373,30 @@ __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t
 }
 
 // the block's window: chunks [first, first + kEgBlock) plus slack, coalesced, then a barrier
+// (NT threads: the single-chain passes run 256, the two-chain ones 128)
+template <uint32_t NT = kEgBlock>
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win, uint64_t first) {
     const uint64_t w0 = (P.start_bit + first * kChunkBits) >> 5;
     // all of a thread's loads in flight at once (clamped, unconditional): the one-word loop under a
     // bounds branch waited out a full global round trip per 256 words, 17 per block
-    constexpr uint32_t kR = (kSyncWinWords + kEgBlock - 1) / kEgBlock;
+    constexpr uint32_t kR = (kSyncWinWords + NT - 1) / NT;
     if (P.n_words) {  // block-uniform
         uint32_t t[kR];
 #pragma unroll
-        for (uint32_t b = 0; b < kR; b++) t[b] = P.words[min(w0 + threadIdx.x + b * kEgBlock, P.n_words - 1)];
+        for (uint32_t b = 0; b < kR; b++) t[b] = P.words[min(w0 + threadIdx.x + b * NT, P.n_words - 1)];
 #pragma unroll
         for (uint32_t b = 0; b < kR; b++) {
-            const uint32_t i = threadIdx.x + b * kEgBlock;
+            const uint32_t i = threadIdx.x + b * NT;
             if (i < kSyncWinWords) win[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
         }
     } else {
-        for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += kEgBlock) win[i] = 0u;
+        for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += NT) win[i] = 0u;
     }
     __syncthreads();
     return LdsBits{win, w0, kSyncWinWords};
 }
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win) {
-    return stage_block_window(P, win, (uint64_t)blockIdx.x * kEgBlock);
+    return stage_block_window<kEgBlock>(P, win, (uint64_t)blockIdx.x * kEgBlock);
 }
 
 // window-relative form of an absolute bit position (clamped: positions past the window behave as the
@@ -421,6 +423,108 @@ __device__ __forceinline__ bool sync_step(WinReader& r, uint32_t stop, uint32_t 
     }
     n++;
     return true;
+}
+
+// The parse passes' chunk interiors: a branchless step (round 4).  The interior loops of round 3 branched
+// per step (refill, run marks, long code, code mark); every branch is exec-mask bookkeeping on the scalar
+// unit and a wave ran each branch any of its lanes took.  Measured (c8, one box, A/B x 2): sync 625 ->
+// 558 us, mark 896 -> 798 us.  Two chunks per thread interleaved through the same step ran slower (739 /
+// 961 us: half the waves, and the compiler did not interleave the chains), not kept.
+// WinReader's state inside a chunk's interior as 32-bit words: bits [pos, pos + avail) left-aligned in
+// hi:lo and zero past avail, the word after them (index nx) in pre; pos = 32 nx - avail.
+struct Lean {
+    uint32_t hi, lo, avail, nx, pre;
+    __device__ __forceinline__ uint32_t pos() const { return nx * 32u - avail; }
+};
+__device__ __forceinline__ Lean lean_from(const WinReader& r) {
+    return Lean{(uint32_t)(r.buf >> 32), (uint32_t)r.buf, (uint32_t)r.avail, r.next, r.pre};
+}
+__device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
+    r.buf = ((uint64_t)c.hi << 32) | c.lo;
+    r.avail = (int)c.avail;
+    r.next = c.nx;
+    r.pos = c.pos();
+    r.pre = r.s[c.nx < r.n ? c.nx : 0u];
+}
+
+// One branchless step inside the interior (every word read lies in the window): a run of 1-bit codes
+// (value 0) of up to 31 -- a run never extends past avail, whose bits are zero -- then a refill to >= 32
+// bits, then the longer code that follows the run if there is one.  Returns the values taken (<= 32);
+// bad: that code has >= 33 bits or 32 leading zeros (left unconsumed for the checked loop).  A run cut
+// short by avail takes no code; the next step continues it.  BOUNDED: room (>= 1) bits are left before
+// the parse's stop; the run ends there at the latest and a code is taken only if it starts before it,
+// so the parse ends exactly at the first code boundary at or past the stop (the code may reach past).
+template <bool BOUNDED = false>
+__device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& bad, uint32_t room = 32u) {
+    // ones at the top of hi, at most 31 (BOUNDED: at most room): the OR-ed bit makes clz defined and caps it
+    const uint32_t cap_bit = BOUNDED ? 0x80000000u >> min(room, 31u) : 1u;
+    uint32_t n1 = __builtin_clz(~c.hi | cap_bit);
+    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
+    c.avail -= n1;
+    // a 0 bit follows the run: a code starts (BOUNDED: before the stop)
+    const bool has = c.avail != 0u && (uint32_t)(b >> 63) == 0u && (!BOUNDED || n1 < room);
+    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
+    // refill: append pre when fewer than 32 bits are buffered (branchless; the re-read of pre is
+    // unconditional, the same word when nothing was appended)
+    const bool need = c.avail < 32u;
+    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
+    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);  // pre << (32 - avail); 0 at avail 0
+    hi = need ? rh : hi;
+    lo = need ? rl : lo;
+    c.avail += need ? 32u : 0u;
+    c.nx += need ? 1u : 0u;
+    c.pre = s[c.nx];
+    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
+    bad = has && zz >= 16u;
+    const bool take = has && zz < 16u;
+    const uint32_t w = take ? 2u * zz + 1u : 0u;
+    b = (((uint64_t)hi << 32) | lo) << w;
+    c.hi = (uint32_t)(b >> 32);
+    c.lo = (uint32_t)b;
+    c.avail -= w;
+    return n1 + (take ? 1u : 0u);
+}
+
+// The resolve walk of chunk t (pass 0 with resolve, below): e = the pass-0 exit of chunk t - 1 (~0u: it
+// ended invalid), s0 = chunk t's pass-0 start, x0 = its pass-0 exit (window-relative), n = its pass-0
+// count, ex = its pass-0 exit (absolute).  On return n / exit are chunk t's true count and exit; true
+// (fail) when the true exit differs from the pass-0 exit that chunk t + 1 was resolved against.
+__device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, uint32_t s0, uint32_t x0, uint32_t stop,
+                                              uint32_t limit, uint64_t base, uint64_t ex, uint32_t& n, uint64_t& exit) {
+    if (e == ~0u) return false;
+    bool met = false;
+    if (e - s0 < kMeetBits) {  // e >= s0: the exit of chunk t - 1 lies at or past its end
+        WinReader a{win, kSyncWinWords, 0, 0, 0, 0, 0};  // pass 0, from s0
+        WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};  // the true parse, from e
+        a.seek(s0);
+        q.seek(e);
+        uint32_t na = 0, nq = 0, code;
+        for (;;) {
+            if (a.pos == q.pos) {  // met: a boundary of both parses
+                met = a.pos <= x0;  // ... at or before the pass-0 exit (else: past the data's end)
+                if (met) n = n - na + nq;
+                break;
+            }
+            if (min(a.pos, q.pos) - s0 >= kMeetBits || max(a.pos, q.pos) > limit) break;
+            const bool adv_a = a.pos < q.pos;  // the one behind takes its next code
+            if (!(adv_a ? a.get(code) : q.get(code))) break;  // 32 zero bits
+            if (adv_a) na++;
+            else nq++;
+        }
+    }
+    if (met) return false;
+    // rare (a dense run of long codes): the confirming pass of this chunk, inline
+    WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};
+    q.seek(e);
+    uint32_t n2 = 0;
+    bool inv2 = false;
+    while (q.pos < stop && sync_step(q, stop, limit, n2, inv2)) {
+    }
+    n = n2;
+    exit = inv2 ? kNoExit : base + q.pos;
+    // chunk t + 1 was resolved against the pass-0 exit: only a different true exit needs the confirming
+    // passes
+    return exit != ex;
 }
 
 // Sync pass.  resolve (pass 0 only): the block owns kEgBlock - 1 chunks, [b * 255, b * 255 + 255), on
@@ -457,16 +561,17 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     if (live) {
         r.seek(s0);
         // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary.
-        // The chunk interior first, without bounds (a step moves at most 64 + 63 bits; as the mark
-        // pass), then the checked steps; an invalid code leaves the lean loop unconsumed.
+        // The chunk interior first, without bounds (a step moves at most 31 + 31 bits), then the checked
+        // steps; a long or invalid code leaves the lean loop unconsumed.
         const uint32_t fast_stop = stop > 128u ? stop - 128u : 0u;
-        while (r.pos < fast_stop) {
-            n += r.ones<true>(64u);
-            if (!r.at_long_code()) continue;  // refill
-            uint32_t code;
-            if (!r.get<true>(code)) break;
-            n++;
-        }
+        // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
+        // chunk end (a code running past the limit is invalid: the checked steps)
+        const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
+        Lean c = lean_from(r);
+        bool bad = false;
+        while (!bad & (c.pos() < fast_stop)) n += lean_step(win, c, bad);
+        while (!bad & (c.pos() < bstop)) n += lean_step<true>(win, c, bad, bstop - c.pos());
+        lean_to(r, c);
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
         }
     }
@@ -481,52 +586,15 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     s_exit[threadIdx.x] = invalid ? ~0u : r.pos;
     __syncthreads();
     if (!live || threadIdx.x == 0) return;  // thread 0: the helper chunk (written by its owner block)
-    bool fail = false;
     uint64_t exit = ex;
-    if (t > 0) {
-        const uint32_t e = s_exit[threadIdx.x - 1];
-        if (e != ~0u) {
-            bool met = false;
-            if (e - s0 < kMeetBits) {  // e >= s0: the exit of chunk t - 1 lies at or past its end
-                WinReader a{win, kSyncWinWords, 0, 0, 0, 0, 0};  // pass 0, from s0
-                WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};  // the true parse, from e
-                a.seek(s0);
-                q.seek(e);
-                uint32_t na = 0, nq = 0, code;
-                for (;;) {
-                    if (a.pos == q.pos) {  // met: a boundary of both parses
-                        met = a.pos <= r.pos;  // ... at or before the pass-0 exit (else: past the data's end)
-                        if (met) n = n - na + nq;
-                        break;
-                    }
-                    if (min(a.pos, q.pos) - s0 >= kMeetBits || max(a.pos, q.pos) > limit) break;
-                    const bool adv_a = a.pos < q.pos;  // the one behind takes its next code
-                    if (!(adv_a ? a.get(code) : q.get(code))) break;  // 32 zero bits
-                    if (adv_a) na++;
-                    else nq++;
-                }
-            }
-            if (!met) {  // rare (a dense run of long codes): the confirming pass of this chunk, inline
-                WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};
-                q.seek(e);
-                uint32_t n2 = 0;
-                bool inv2 = false;
-                while (q.pos < stop && sync_step(q, stop, limit, n2, inv2)) {
-                }
-                n = n2;
-                exit = inv2 ? kNoExit : base + q.pos;
-                // chunk t + 1 was resolved against the pass-0 exit: only a different true exit needs
-                // the confirming passes
-                fail = exit != ex;
-            }
-        }
-    }
+    const bool fail = t > 0 && resolve_chunk(win, s_exit[threadIdx.x - 1], s0, r.pos, stop, limit, base, ex, n, exit);
     P.exit_out[t] = exit;
     P.count[t] = n;
     const uint64_t fb = __ballot(fail);
     if (fb != 0ull && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(fb)) atomicOr((unsigned int*)&P.status[0], 1u);
 }
 
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     __shared__ uint32_t win[kSyncWinWords];
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
@@ -536,8 +604,17 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned int*)&P.status[2], 4u);
         return;
     }
+    const uint64_t first = (uint64_t)blockIdx.x * kEgBlock;
+    // (the per-chunk loads below issued before the window's staging instead measured 633 -> 745 us)
     const LdsBits L = stage_block_window(P, win);
-    const uint64_t t = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
+    // the interior's marks leave through a buffer descriptor based at the block's first mark (block-
+    // uniform: marks of its chunks have index >= off[first] / 32); a step without a mark aims its store
+    // past the range, where it is dropped -- no branch
+    const uint64_t n_marks = P.n_values / kMarkVals + 1;  // the mark buffer's size (eg_decode_front)
+    const uint64_t m_lo = min(P.off[first], P.n_values) / kMarkVals;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.mark + m_lo, (short)0,
+                                                        (int)min((n_marks - m_lo) * 8u, (uint64_t)0x7FFFFFF0u), 0x00020000);
+    const uint64_t t = first + threadIdx.x;
     if (t >= P.n_chunks) return;
     const uint64_t idx0 = P.off[t];
     if (idx0 >= P.n_values) return;
@@ -558,26 +635,37 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
     uint64_t* const mk = P.mark + (idx0 / kMarkVals);  // mark[(idx0 + i) / 32] = mk[(ph + i) / 32]
     uint32_t i = 0, code;
-    // Interior of the chunk: a step moves at most 64 + 63 bits and 65 values, so while the parse is
+    // Interior of the chunk: a step moves at most 31 + 31 bits and 32 values, so while the parse is
     // 128 bits short of the chunk end and of the data limit, and 66 values short of the wanted count,
-    // none of the bounds below can bind -- a lean loop without them (a 32-zero-bit invalid code leaves
-    // it for the checked loop, which reports it).
+    // none of the bounds below can bind -- a lean loop without them (a long or invalid code leaves it for
+    // the checked loop, which reads or reports it).
     const uint32_t lim_end = min(end, limit);
     const uint32_t fast_end = lim_end > 128u ? lim_end - 128u : 0u;
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
-    while (r.pos < fast_end && i < fast_rem) {
-        const uint32_t p0 = r.pos;
-        const uint32_t k = r.ones<true>(64u);
-        // the run's marks: values i + d0 and i + d0 + 32 (a run of <= 64 holds at most two)
-        const uint32_t d0 = (kMarkVals - ((ph + i) & (kMarkVals - 1))) & (kMarkVals - 1);
-        if (d0 < k) mk[(ph + i + d0) / kMarkVals] = base + p0 + d0;
-        if (d0 + kMarkVals < k) mk[(ph + i + d0) / kMarkVals + 1] = base + p0 + d0 + kMarkVals;
-        i += k;
-        if (!r.at_long_code()) continue;  // refill
-        const uint32_t p1 = r.pos;
-        if (!r.get<true>(code)) break;  // invalid: nothing consumed, the checked loop reports it
-        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p1;
-        i++;
+    {
+        const uint32_t mb = (uint32_t)(idx0 / kMarkVals - m_lo);  // this chunk's first mark, block-relative
+        Lean c = lean_from(r);
+        bool bad = false;
+        // a step takes nv <= 32 values, value i + d at bit p0 + d: at most one mark, value i + d0
+        auto mark = [&](uint32_t p0, uint32_t nv) {
+            const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
+            const uint32_t o = d0 < nv ? (mb + (ph + i + d0) / kMarkVals) * 8u : 0x80000000u;
+            const uint64_t v = base + (p0 + d0);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, rsrc, (int)o, 0, 0);
+            i += nv;
+        };
+        while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
+            const uint32_t p0 = c.pos();
+            mark(p0, lean_step(win, c, bad));
+        }
+        // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
+        // end take the checked steps)
+        const uint32_t bend = limit >= end + 64u ? end : 0u;
+        while (!bad & (c.pos() < bend) & (i < fast_rem)) {
+            const uint32_t p0 = c.pos();
+            mark(p0, lean_step<true>(win, c, bad, bend - p0));
+        }
+        lean_to(r, c);
     }
     while (i < rem && r.pos < end) {
         const uint32_t p0 = r.pos;

@@ -122,26 +122,16 @@ struct WinReader {
         next = k + 2;
         pre = s[next < n ? next : 0u];
     }
-    // LEAN: the parse stands >= 128 bits before the window's end (the passes' lean interior loops), so
-    // every word read lies inside the window: no bounds selects
-    template <bool LEAN = false>
     __device__ __forceinline__ void refill() {
         if (avail <= 32) {
-            if constexpr (LEAN) {
-                buf |= (uint64_t)pre << (32 - avail);
-                avail += 32;
-                pre = s[++next];
-            } else {
-                buf |= (uint64_t)(next < n ? pre : 0u) << (32 - avail);
-                avail += 32;
-                ++next;
-                pre = s[next < n ? next : 0u];
-            }
+            buf |= (uint64_t)(next < n ? pre : 0u) << (32 - avail);
+            avail += 32;
+            ++next;
+            pre = s[next < n ? next : 0u];
         }
     }
-    template <bool LEAN = false>
     __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
-        refill<LEAN>();
+        refill();
         const uint64_t inv = ~buf;
         uint32_t n1 = inv ? (uint32_t)__clzll((long long)inv) : 64u;
         n1 = min(min(n1, (uint32_t)avail), maxn);
@@ -151,9 +141,8 @@ struct WinReader {
         return n1;
     }
     __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
-    template <bool LEAN = false>
     __device__ __forceinline__ bool get(uint32_t& code) {
-        refill<LEAN>();
+        refill();
         const uint32_t hi32 = (uint32_t)(buf >> 32);
         if (hi32 == 0u) return false;  // 32 zero bits: invalid
         const int width = 2 * __builtin_clz(hi32) + 1;
