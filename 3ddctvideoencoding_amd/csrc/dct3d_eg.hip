@@ -257,24 +257,30 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
 }
 
 // Fused path, K3: one wave per segment (8 cubes coded by encode_eg_kernel, lane l's words at rows
-// i*64 + l of the slot).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
+// i*64 + l of the slot; a lane-major slot measured K1 2.06 -> 2.21 ms and this kernel 0.28 -> 0.98 ms).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
 // shifted into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane
 // has >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
-// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.  The first 4 rows are loaded
-// before any is used (typical content needs <= 3 words per lane).
+// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.  The first kCompactPF rows are loaded
+// before any is used, the next kCompactPF while they are placed.  The interior words are placed in a
+// wave-private LDS image of the segment and leave as whole consecutive words, lane j storing words j,
+// j + 64, ... (round 4: stored straight from the lanes, each store instruction hit 64 scattered partial
+// lines); a segment longer than the image (never for 8-bit content) stores straight from the lanes.
+constexpr uint32_t kCompactImg = 1024;  // words per wave (a typical segment: ~180)
+constexpr int kCompactPF = 4;            // rows per load round trip (8: no gain)
 __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
                                                               const uint16_t* __restrict__ lane_bits, uint32_t seg_cap) {
+    __shared__ uint32_t s_img[kEgWaves][kCompactImg];
     if (P.status[1] != 0) return;  // capacity failure: nothing is written
     const int lane = threadIdx.x & 63;
     const uint64_t s = (uint64_t)blockIdx.x * kEgWaves + (threadIdx.x >> 6);
     if (s >= P.n_cubes) return;
     // wave-uniform (scalar) bases with 32-bit lane offsets: the segment's slot and its first output word
     const uint32_t* seg = slot + (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)s) * seg_cap;
-    // independent loads, one round trip: the first 4 rows unconditionally (a slot has >= 27 rows;
-    // words past a lane's last one are never used), its bit count, the segment offset
-    uint32_t pre[4];
+    // independent loads, one round trip: the first rows unconditionally (a slot has >= 27 rows; words
+    // past a lane's last one are never used), its bit count, the segment offset
+    uint32_t buf[kCompactPF];
 #pragma unroll
-    for (int t = 0; t < 4; t++) pre[t] = seg[t * 64 + lane];
+    for (int t = 0; t < kCompactPF; t++) buf[t] = seg[t * 64 + lane];
     const uint32_t lb = lane_bits[s * 64 + lane];
     const uint64_t base = P.off[s];
     uint32_t* const outs = P.out + (base >> 5);
@@ -293,19 +299,27 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
     const uint32_t nlb = __shfl_down(lb, 1, 64);
     const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
     const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
+    // the segment's words relative to its first one (base >> 5): [0, nimg); 0 and nimg - 1 are head / tail
+    const uint32_t tot = __shfl(incl, 63, 64);
+    const uint32_t nimg = tot ? (uint32_t)(((base + tot - 1) >> 5) - (base >> 5) + 1) : 0u;
+    const bool staged = nimg <= kCompactImg;  // wave-uniform
+    uint32_t* const img = s_img[threadIdx.x >> 6];
+    auto put = [&](uint32_t rel, uint32_t v) {  // an interior word, rel in [1, nimg - 1)
+        if (staged) img[rel] = v;
+        else outs[rel] = v;
+    };
     uint32_t prev = 0, first = 0, last = 0;
-    uint32_t buf[4] = {pre[0], pre[1], pre[2], pre[3]};
-    for (uint32_t d0 = 0; d0 < ndst; d0 += 4) {
-        // rows d0 + 4 .. d0 + 7 in flight while rows d0 .. d0 + 3 are placed: a dense lane (the
-        // low-frequency part of a cube: up to 54 rows) waits one load round trip per 4 rows, not per row
-        uint32_t nxt[4];
+    for (uint32_t d0 = 0; d0 < ndst; d0 += kCompactPF) {
+        // the next rows in flight while these are placed: a dense lane (the low-frequency part of a
+        // cube: up to 54 rows) waits one load round trip per kCompactPF rows, not per row
+        uint32_t nxt[kCompactPF];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const uint32_t d = d0 + 4 + t;
+        for (int t = 0; t < kCompactPF; t++) {
+            const uint32_t d = d0 + kCompactPF + t;
             nxt[t] = d < nsrc ? seg[d * 64u + (uint32_t)lane] : 0u;
         }
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
+        for (int t = 0; t < kCompactPF; t++) {
             const uint32_t d = d0 + t;
             if (d < ndst) {
                 const uint32_t cur = d < nsrc ? buf[t] : 0u;
@@ -313,26 +327,32 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
                 prev = cur;
                 if (d == 0) first = v;
                 if (d == ndst - 1) last = v;
-                if (d != 0 && d != ndst - 1) outs[wrel + d] = __builtin_bswap32(v);
+                if (d != 0 && d != ndst - 1) put(wrel + d, __builtin_bswap32(v));
             }
         }
 #pragma unroll
-        for (int t = 0; t < 4; t++) buf[t] = nxt[t];
+        for (int t = 0; t < kCompactPF; t++) buf[t] = nxt[t];
     }
     const uint32_t nfirst = __shfl_down(first, 1, 64);
     if (next_shares) last |= nfirst;  // ndst == 1 only when r == 0 and lb == 32: never shared then
-    if (ndst == 0) return;
-    const bool shares_prev = lane > 0 && r != 0;  // my first word belongs to lane - 1's last store
-    if (ndst == 1) {
-        if (lane == 0) P.head[s] = __builtin_bswap32(first);
-        else if (last_lane) P.tail[s] = __builtin_bswap32(last);
-        else P.out[w0] = __builtin_bswap32(last);
-        return;
+    if (ndst != 0) {
+        const bool shares_prev = lane > 0 && r != 0;  // my first word belongs to lane - 1's last store
+        if (ndst == 1) {
+            if (lane == 0) P.head[s] = __builtin_bswap32(first);
+            else if (last_lane) P.tail[s] = __builtin_bswap32(last);
+            else put(wrel, __builtin_bswap32(last));
+        } else {
+            if (lane == 0) P.head[s] = __builtin_bswap32(first);
+            else if (!shares_prev) put(wrel, __builtin_bswap32(first));
+            if (last_lane) P.tail[s] = __builtin_bswap32(last);
+            else put(wrel + ndst - 1, __builtin_bswap32(last));
+        }
     }
-    if (lane == 0) P.head[s] = __builtin_bswap32(first);
-    else if (!shares_prev) P.out[w0] = __builtin_bswap32(first);
-    if (last_lane) P.tail[s] = __builtin_bswap32(last);
-    else P.out[w0 + ndst - 1] = __builtin_bswap32(last);
+    if (!staged || nimg < 3) return;  // wave-uniform
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i = 1 + (uint32_t)lane; i + 1 < nimg; i += 64) outs[i] = img[i];
 }
 
 // =================================================================================================
