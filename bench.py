@@ -404,7 +404,9 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    # DCT3D_BENCH_FORCE_DIST=1: the distributed path (process group, barrier, all-gathers, RCCL) even for a
+    # single rank, so that a one-GPU box runs the code the driver's N > 1 runs (tests/test_gpu_bench_flow.py)
+    if world > 1 or os.environ.get("DCT3D_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         # one process per GPU over RCCL ("nccl").  DCT3D_BENCH_BACKEND=gloo rehearses the N>1 flow with
         # several ranks on fewer GPUs (ranks are mapped onto the visible devices round-robin).

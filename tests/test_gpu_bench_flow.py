@@ -55,3 +55,23 @@ def test_two_rank_bench_line(config, args, scaling):
         assert cubes == 4 * (3840 // 8) * (2160 // 8)
     # value = every rank's cubes per step over the slowest rank's time per step
     assert abs(d["value"] - cubes / (d["ms_per_step"] * 1e-3)) <= 1e-6 * d["value"]
+
+
+def test_rccl_path_single_rank():
+    """The RCCL ("nccl") branch of the N > 1 flow -- init_process_group with the rank's device, barrier,
+    the per-rank all_gather, the max / sum all-reduces and the --xgmi leg's collectives -- executed for
+    real on the box's one GPU as a one-rank job (DCT3D_BENCH_FORCE_DIST=1; RCCL takes one GPU per rank,
+    so two ranks on one GPU can only rehearse over gloo, above)."""
+    env = dict(os.environ, DCT3D_BENCH_FORCE_DIST="1", DCT3D_BENCH_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "1", "--steps", "3", "--warmup", "1", "--settle-ms", "0", "--no-cpu-baseline",
+           "--no-ceiling", "--stacks", "4", "--xgmi"]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert [p["rank"] for p in d["per_rank"]] == [0]
+    assert d["xgmi"] is not None and d["xgmi"]["verified"]
