@@ -614,9 +614,16 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     if (fb != 0ull && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(fb)) atomicOr((unsigned int*)&P.status[0], 1u);
 }
 
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// The chunk's marks are collected in LDS (2 bytes each, relative to the chunk's true start, in the
+// thread's own slot of kMkSlot entries) and written out at the end, each thread its consecutive marks back
+// to back, so that the L2 assembles whole lines: WRITE_SIZE 1.67 GB -> 0.52 GB (the marks' own bytes) and
+// the pass 708 -> 529 us on one box (round 4; stored one at a time as the parse reached them, through a
+// buffer descriptor, each lane's marks tens of microseconds apart, the lines were written back partial).
+// The slots cost 9 KiB per block (6 blocks per CU instead of 8).
+constexpr uint32_t kMkSlot = 18;  // a chunk has at most 17 marks (<= 512 values); entry 17: the dummy
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     __shared__ uint32_t win[kSyncWinWords];
+    __shared__ uint16_t s_mk[kEgBlock * kMkSlot];
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
     // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
     // (status[2] != 0) and the host reruns without speculation
@@ -627,13 +634,6 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint64_t first = (uint64_t)blockIdx.x * kEgBlock;
     // (the per-chunk loads below issued before the window's staging instead measured 633 -> 745 us)
     const LdsBits L = stage_block_window(P, win);
-    // the interior's marks leave through a buffer descriptor based at the block's first mark (block-
-    // uniform: marks of its chunks have index >= off[first] / 32); a step without a mark aims its store
-    // past the range, where it is dropped -- no branch
-    const uint64_t n_marks = P.n_values / kMarkVals + 1;  // the mark buffer's size (eg_decode_front)
-    const uint64_t m_lo = min(P.off[first], P.n_values) / kMarkVals;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(P.mark + m_lo, (short)0,
-                                                        (int)min((n_marks - m_lo) * 8u, (uint64_t)0x7FFFFFF0u), 0x00020000);
     const uint64_t t = first + threadIdx.x;
     if (t >= P.n_chunks) return;
     const uint64_t idx0 = P.off[t];
@@ -645,7 +645,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
     const uint32_t limit = rel_bit(P.limit_bit, base);
     WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
-    r.seek(rel_bit(s, base));
+    const uint32_t sp = rel_bit(s, base);  // the chunk's true start (LDSM marks are relative to it)
+    r.seek(sp);
+    uint16_t* const myk = s_mk + threadIdx.x * kMkSlot;  // mark k of the chunk (value 32 k - ph) at myk[k]
     // chunk-relative 32-bit value count i (value idx0 + i): the 64-bit index arithmetic per step was a
     // large part of the pass.  A chunk holds at most ~kChunkBits + 64 codes, so rem below never binds
     // unless the wanted values end inside this chunk.
@@ -663,15 +665,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t fast_end = lim_end > 128u ? lim_end - 128u : 0u;
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
     {
-        const uint32_t mb = (uint32_t)(idx0 / kMarkVals - m_lo);  // this chunk's first mark, block-relative
         Lean c = lean_from(r);
         bool bad = false;
         // a step takes nv <= 32 values, value i + d at bit p0 + d: at most one mark, value i + d0
         auto mark = [&](uint32_t p0, uint32_t nv) {
             const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
-            const uint32_t o = d0 < nv ? (mb + (ph + i + d0) / kMarkVals) * 8u : 0x80000000u;
-            const uint64_t v = base + (p0 + d0);
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, rsrc, (int)o, 0, 0);
+            myk[d0 < nv ? (ph + i + d0) / kMarkVals : kMkSlot - 1] = (uint16_t)(p0 + d0 - sp);  // no branch
             i += nv;
         };
         while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
@@ -700,7 +699,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
         const uint32_t k = r.ones(min(room, 64u));
         if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
             for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
-                mk[(ph + j) / kMarkVals] = base + p0 + (j - i);
+                myk[(ph + j) / kMarkVals] = (uint16_t)(p0 + (j - i) - sp);
             i += k;
             if (ends_here && i == rem) P.status[1] = base + r.pos;  // the bit after the last wanted value
         }
@@ -712,9 +711,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
             atomicOr((unsigned int*)&P.status[2], (uint64_t)p1 + 32 <= limit && r.pos <= limit ? 1u : 2u);
             return;
         }
-        if (((ph + i) & (kMarkVals - 1)) == 0) mk[(ph + i) / kMarkVals] = base + p1;
+        if (((ph + i) & (kMarkVals - 1)) == 0) myk[(ph + i) / kMarkVals] = (uint16_t)(p1 - sp);
         if (++i == rem && ends_here) P.status[1] = base + r.pos;
     }
+    // the chunk's marks k = (ph ? 1 : 0) .. (ph + i - 1) / 32, back to back
+    const uint64_t b0 = base + sp;
+    for (uint32_t k = ph ? 1u : 0u; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) mk[k] = b0 + myk[k];
 }
 
 template <int D>
