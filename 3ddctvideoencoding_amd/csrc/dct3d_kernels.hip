@@ -33,14 +33,43 @@ namespace dct3d {
 // by Parseval, DC included).  Then lane (c', part) codes stream positions part*VPL .. part*VPL+VPL-1
 // of cube c' (diagonal-slice order, CubeUtils.c:5-46; signed order-0 Exp-Golomb, ExpGolomb.c:32-64)
 // into its own words of the segment's slot; eg_compact_kernel later concatenates the lanes.
-// signed order-0 Exp-Golomb code of the int16 value in the low half of x (ExpGolomb.c:32-64):
-// v <= 0 -> 1 - 2v, v > 0 -> 2v; width = 2 * bit_length(code) - 1
-__device__ __forceinline__ uint32_t eg_code16(uint32_t x, uint32_t& width) {
-    const int32_t v = (int32_t)(int16_t)(uint16_t)x;
-    const uint32_t ng = (uint32_t)(-v);
-    const uint32_t code = ((ng << 1) ^ (uint32_t)((int32_t)ng >> 31)) + 1u;
-    width = 63u - 2u * (uint32_t)__builtin_clz(code);  // code >= 1: a plain v_ffbh_u32 (no zero case)
-    return code;
+// Signed order-0 Exp-Golomb (ExpGolomb.c:32-64): v <= 0 -> 1 - 2v, v > 0 -> 2v = max(2v, 1 - 2v); the
+// code's width is 2 * bit_length(code) - 1.  K1 stages the codes, not the values: two per register
+// through packed 16-bit ops (|v| <= 255*sqrt(512) < 2^13, so 2v and 1 - 2v fit int16).
+typedef short eg_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t eg_code_pair(uint32_t hi, uint32_t lo) {
+    const eg_s16x2 v = __builtin_bit_cast(eg_s16x2, __builtin_amdgcn_perm(hi, lo, 0x05040100u));
+    const eg_s16x2 t = v + v;
+    const eg_s16x2 c = __builtin_elementwise_max(t, (eg_s16x2)(1) - t);
+    return __builtin_bit_cast(uint32_t, c);
+}
+// The code's width, 63 - 2*clz(code), as one v_mad_i32_i24 (the compiler would split it into a shift
+// and an xor); code >= 1: a plain v_ffbh_u32
+__device__ __forceinline__ uint32_t eg_width(uint32_t code) {
+    uint32_t w;
+    asm("v_mad_i32_i24 %0, %1, -2, 63" : "=v"(w) : "v"((uint32_t)__builtin_clz(code)));
+    return w;
+}
+// g << w, then code OR-ed into the low word (a 32-bit OR: the code's upper bits are known zero there)
+__device__ __forceinline__ uint64_t eg_push(uint64_t g, uint32_t w, uint32_t code) {
+    const uint64_t t = g << (w & 63u);
+    return ((uint64_t)(uint32_t)(t >> 32) << 32) | (uint32_t)((uint32_t)t | code);
+}
+
+// Append W < 64 stream bits (the low W bits of g, MSB first) to a lane's pending bits (p: the low nb <
+// 32 bits, nothing above them), branch-free.  The words completed (0, 1 or 2) go to the lane's next slot
+// rows through the segment's buffer descriptor (a lane without a word stores out of range: dropped);
+// the bits left pending are the low T mod 32 bits of p * 2^W + g.
+__device__ __forceinline__ void eg_append(uint64_t g, uint32_t W, uint32_t& p, uint32_t& nb,
+                                          __amdgpu_buffer_rsrc_t seg, uint32_t& dofs) {
+    const uint32_t T = nb + W;
+    const uint32_t w0 = (p << ((32u - nb) & 31u)) | (uint32_t)(g >> ((T - 32u) & 63u));
+    const uint32_t w1 = (uint32_t)(g >> ((T - 64u) & 63u));
+    __builtin_amdgcn_raw_buffer_store_b32(w0, seg, (int)(T >= 32u ? dofs : 0x80000000u), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w1, seg, (int)(T >= 64u ? dofs + 256u : 0x80000000u), 0, 0);
+    dofs += (T >> 5) << 8;
+    p = __builtin_amdgcn_ubfe((uint32_t)((uint64_t)p << W) | (uint32_t)g, 0u, T & 31u);
+    nb = T & 31u;
 }
 
 template <int D>
@@ -130,18 +159,15 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     }
     if (!valid) fm_lo = fm_hi = 0;
 
-    // stage the cubes as int16, cube-major (k = (kz*8 + ky)*8 + kx at byte 2k of cube c)
+    // stage the cubes' Exp-Golomb codes as uint16, cube-major (k = (kz*8 + ky)*8 + kx at byte 2k of cube c)
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
         char* row = wl + c * CUBE_B + 2 * ((kz * 8 + ky) * 8 + kx0);
         if constexpr (D == 8) {
-            *(uint4*)row = make_uint4(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
-                                      __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u),
-                                      __builtin_amdgcn_perm(qv[ky][5], qv[ky][4], 0x05040100u),
-                                      __builtin_amdgcn_perm(qv[ky][7], qv[ky][6], 0x05040100u));
+            *(uint4*)row = make_uint4(eg_code_pair(qv[ky][1], qv[ky][0]), eg_code_pair(qv[ky][3], qv[ky][2]),
+                                      eg_code_pair(qv[ky][5], qv[ky][4]), eg_code_pair(qv[ky][7], qv[ky][6]));
         } else {
-            *(uint2*)row = make_uint2(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
-                                      __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u));
+            *(uint2*)row = make_uint2(eg_code_pair(qv[ky][1], qv[ky][0]), eg_code_pair(qv[ky][3], qv[ky][2]));
         }
     }
     wave_lds_sync();
@@ -160,7 +186,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
             const int skz = (D == 8) ? sj : (sj >> 1), skx0 = (D == 8) ? 0 : (sj & 1) * 4;
             const uint32_t k = (uint32_t)((skz * 8 + bit / NB) * 8 + skx0 + bit % NB);
             const int q = exact_coef<D>(R, cube0 + sc, k, lane, (int*)rs, (double*)(rs + kMaxGroupsDev * 4));
-            if (lane == 0) *(int16_t*)(wl + sc * CUBE_B + 2 * k) = (int16_t)q;
+            if (lane == 0) *(uint16_t*)(wl + sc * CUBE_B + 2 * k) = (uint16_t)(q > 0 ? 2 * q : 1 - 2 * q);
             if (lane == src) {
                 if (fm_lo) fm_lo &= fm_lo - 1;
                 else fm_hi &= fm_hi - 1;
@@ -170,40 +196,44 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     }
 
     // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp, read from the
-    // staged cube, with a 64-bit accumulator: one MSB-first word out whenever 32 bits are pending
-    // (width <= 27, + 31 pending), word i of lane l at slot row i (i*64 + l).  eg_compact_kernel
-    // concatenates the lanes.  (Buffering the words in LDS first needs the values in registers to
-    // free the region: +6 % kernel time for the pack / unpack, more than the scattered stores cost.)
+    // staged codes 8 at a time: the 8 codes concatenated into one 64-bit group when they fit (W < 64;
+    // else one by one), each group appended to the lane's pending bits with at most two words out, word
+    // i of lane l at slot row i (i*64 + l).  eg_compact_kernel concatenates the lanes.  (Buffering the
+    // words in LDS first needs the values in registers to free the region: +6 % kernel time for the pack
+    // / unpack, more than the scattered stores cost.)
     const int cp = lane >> 3, part = lane & 7;
     const bool lvalid = cube0 + cp < P.n_cubes;
     const char* cb = wl + cp * CUBE_B;
-    // the segment's slot base is wave-uniform (scalar); each store adds a 32-bit lane offset
-    char* const seg = (char*)(E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap);
+    // the segment's slot (wave-uniform base and size) as a buffer descriptor; each store adds a 32-bit
+    // lane offset
+    const __amdgpu_buffer_rsrc_t seg = __builtin_amdgcn_make_buffer_rsrc(
+        E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap, (short)0, (int)(E.seg_cap * 4u), 0x00020000);
     uint32_t dofs = (uint32_t)lane * 4u;  // byte offset of the lane's next word: (nw * 64 + lane) * 4
-    uint64_t acc = 0;
-    uint32_t nb = 0;
+    uint32_t p = 0, nb = 0;
     if (lvalid) {
 #pragma unroll 1
         for (int i0 = 0; i0 < VPL; i0 += 8) {
             const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
             const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
-            uint32_t v[8];
+            uint32_t cd[8], w[8];
 #pragma unroll
-            for (int e = 0; e < 8; e++) v[e] = *(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
+            for (int e = 0; e < 8; e++) cd[e] = *(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
+            uint64_t g = 0;
+            uint32_t W = 0;
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                uint32_t width;
-                const uint32_t code = eg_code16(v[e], width);
-                acc = (acc << width) | code;
-                nb += width;
-                if (nb >= 32u) {
-                    nb -= 32u;
-                    *(uint32_t*)(seg + dofs) = (uint32_t)(acc >> nb);
-                    dofs += 256u;
-                }
+                w[e] = eg_width(cd[e]);
+                g = eg_push(g, w[e], cd[e]);
+                W += w[e];
+            }
+            if (__builtin_expect(W < 64u, 1)) {
+                eg_append(g, W, p, nb, seg, dofs);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; e++) eg_append(cd[e], w[e], p, nb, seg, dofs);
             }
         }
-        if (nb) *(uint32_t*)(seg + dofs) = (uint32_t)(acc << (32u - nb));
+        __builtin_amdgcn_raw_buffer_store_b32(p << ((32u - nb) & 31u), seg, (int)(nb ? dofs : 0x80000000u), 0, 0);
     }
     const uint32_t nw = (dofs - (uint32_t)lane * 4u) >> 8;  // full words stored
     const uint32_t lbits = lvalid ? nw * 32u + nb : 0u;
