@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
 }
 
 // Fused path, K3: one wave per segment (8 cubes coded by encode_eg_kernel, lane l's words at rows
-// i*64 + l of the slot; a lane-major slot measured K1 2.06 -> 2.21 ms and this kernel 0.28 -> 0.98 ms).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
+// i*64 + eg_slot_col(l) of the slot; a lane-major slot measured K1 2.06 -> 2.21 ms and this kernel 0.28 -> 0.98 ms).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
 // shifted into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane
 // has >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
 // head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.  The first kCompactPF rows are loaded
@@ -279,8 +279,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
     // independent loads, one round trip: the first rows unconditionally (a slot has >= 27 rows; words
     // past a lane's last one are never used), its bit count, the segment offset
     uint32_t buf[kCompactPF];
+    const uint32_t col = eg_slot_col((uint32_t)lane);
 #pragma unroll
-    for (int t = 0; t < kCompactPF; t++) buf[t] = seg[t * 64 + lane];
+    for (int t = 0; t < kCompactPF; t++) buf[t] = seg[t * 64 + col];
     const uint32_t lb = lane_bits[s * 64 + lane];
     const uint64_t base = P.off[s];
     uint32_t* const outs = P.out + (base >> 5);
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 #pragma unroll
         for (int t = 0; t < kCompactPF; t++) {
             const uint32_t d = d0 + kCompactPF + t;
-            nxt[t] = d < nsrc ? seg[d * 64u + (uint32_t)lane] : 0u;
+            nxt[t] = d < nsrc ? seg[d * 64u + col] : 0u;
         }
 #pragma unroll
         for (int t = 0; t < kCompactPF; t++) {

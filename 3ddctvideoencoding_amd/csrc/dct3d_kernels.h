@@ -112,13 +112,18 @@ struct EgDecParams {
 // certify, the exact Java replay of uncertified coefficients inside the wave, then the wave's 8
 // cubes coded straight into a private slot (no int32 cube-major round trip).  Segment = one wave = 8
 // consecutive cubes; lane l codes 1/8 of one cube's diagonal stream into its words of the slot.
+// Column of coding lane l = (cube c, part) in a slot row: part-major (part * 8 + c), so that the 8
+// low-frequency lanes (part 0, the most words) share one 32-byte piece of each row past the short
+// lanes' last word instead of touching four 64-byte lines of it.
+__host__ __device__ constexpr uint32_t eg_slot_col(uint32_t l) { return (l & 7u) * 8u + (l >> 3); }
+
 struct EgFusedParams {
     const int32_t* ngroups;    // exact replay tables (as EncodeParams)
     const double* coef;
     const uint8_t* group_of;
     const uint16_t* diag;      // [cs] stream position -> cube index
-    uint32_t* slot;            // [n_seg * seg_cap]: word i of lane l at i*64 + l, MSB-first, each lane's
-                               // first bit at bit 31 of its word 0
+    uint32_t* slot;            // [n_seg * seg_cap]: word i of lane l at i*64 + eg_slot_col(l), MSB-first,
+                               // each lane's first bit at bit 31 of its word 0
     uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
     uint16_t* lane_bits;       // [n_seg * 64] bits coded by each lane
     uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)

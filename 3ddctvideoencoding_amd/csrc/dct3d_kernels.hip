@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp, read from the
     // staged codes 8 at a time: the 8 codes concatenated into one 64-bit group when they fit (W < 64;
     // else one by one), each group appended to the lane's pending bits with at most two words out, word
-    // i of lane l at slot row i (i*64 + l).  eg_compact_kernel concatenates the lanes.  (Buffering the
+    // i of lane l at slot row i (i*64 + eg_slot_col(l)).  eg_compact_kernel concatenates the lanes.  (Buffering the
     // words in LDS first needs the values in registers to free the region: +6 % kernel time for the pack
     // / unpack, more than the scattered stores cost.)
     const int cp = lane >> 3, part = lane & 7;
@@ -208,7 +208,8 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     // lane offset
     const __amdgpu_buffer_rsrc_t seg = __builtin_amdgcn_make_buffer_rsrc(
         E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap, (short)0, (int)(E.seg_cap * 4u), 0x00020000);
-    uint32_t dofs = (uint32_t)lane * 4u;  // byte offset of the lane's next word: (nw * 64 + lane) * 4
+    const uint32_t col4 = eg_slot_col((uint32_t)lane) * 4u;
+    uint32_t dofs = col4;  // byte offset of the lane's next word: (nw * 64 + col) * 4
     uint32_t p = 0, nb = 0;
     if (lvalid) {
 #pragma unroll 1
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
         }
         __builtin_amdgcn_raw_buffer_store_b32(p << ((32u - nb) & 31u), seg, (int)(nb ? dofs : 0x80000000u), 0, 0);
     }
-    const uint32_t nw = (dofs - (uint32_t)lane * 4u) >> 8;  // full words stored
+    const uint32_t nw = (dofs - col4) >> 8;  // full words stored
     const uint32_t lbits = lvalid ? nw * 32u + nb : 0u;
     E.lane_bits[(size_t)wid * 64 + lane] = (uint16_t)lbits;
     uint32_t tot = lbits;

@@ -1,7 +1,8 @@
 /* main.c -- CLI with the reference's argument convention (main.c:5-49):
  *   dct3d_codec list_devices
  *   dct3d_codec encode|decode <input> <output> <width> <height> <frames> [device_index (1-based)] [block_depth 8|4]
- * (list_platforms is accepted as an alias of list_devices.) */
+ * (list_platforms is accepted as an alias of list_devices.)  device_index may be a comma-separated list
+ * ("1,2,3"): encode_multi / decode_multi over those devices. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -13,7 +14,8 @@ static void usage(void) {
     printf("Usage\n\n");
     printf("dct3d_codec list_devices -> List available HIP devices\n");
     printf("dct3d_codec encode|decode <input file> <output file> <width> <height> <nr of frames> "
-           "<device_index (optional, 1-based)> <block depth 8|4 (optional)> -> Encode/Decode given file\n");
+           "<device_index (optional, 1-based; a list a,b,... uses several)> <block depth 8|4 (optional)> -> "
+           "Encode/Decode given file\n");
 }
 
 int main(int argc, char *argv[]) {
@@ -38,10 +40,23 @@ int main(int argc, char *argv[]) {
         return 1;
     }
     const int width = atoi(argv[4]), height = atoi(argv[5]), frames = atoi(argv[6]);
-    const int dev = argc > 7 ? atoi(argv[7]) : 1;
+    int devs[64], n_dev = 0;
+    if (argc > 7) {
+        for (const char *p = argv[7]; *p && n_dev < 64;) {
+            devs[n_dev++] = atoi(p);
+            const char *c = strchr(p, ',');
+            if (!c) break;
+            p = c + 1;
+        }
+    }
+    if (n_dev == 0) devs[n_dev++] = 1;
     const int depth = argc > 8 ? atoi(argv[8]) : DCT_BLOCK_DEPTH;
-    if (!strcmp(argv[1], "encode")) return encode_ex(argv[2], argv[3], width, height, frames, dev, depth, 0);
-    if (!strcmp(argv[1], "decode")) return decode_ex(argv[2], argv[3], width, height, frames, dev, depth, 0);
+    if (!strcmp(argv[1], "encode"))
+        return n_dev > 1 ? encode_multi(argv[2], argv[3], width, height, frames, devs, n_dev, depth, 0)
+                         : encode_ex(argv[2], argv[3], width, height, frames, devs[0], depth, 0);
+    if (!strcmp(argv[1], "decode"))
+        return n_dev > 1 ? decode_multi(argv[2], argv[3], width, height, frames, devs, n_dev, depth, 0)
+                         : decode_ex(argv[2], argv[3], width, height, frames, devs[0], depth, 0);
     usage();
     return 1;
 }

@@ -38,6 +38,52 @@ def test_cli_encode_decode(pkg, plan8, tmp_path, w, h, frames, kind, host_eg, ba
     assert np.array_equal(dec, plan8.decode_q(q.reshape(-1, 8, 8, 8), w, h, n_stacks * 8))
 
 
+@pytest.mark.parametrize("devices,batch", [("1,1", "1"), ("1,1,1", "2"), ("1,1", "16")])
+@pytest.mark.parametrize("w,h,frames,kind", [(64, 64, 40, "ramp"), (320, 240, 24, "uniform")])
+def test_cli_multi_device(pkg, plan8, tmp_path, w, h, frames, kind, devices, batch):
+    """encode_multi / decode_multi (a device list; one box has one GPU, so the list repeats it: one
+    context and host thread per entry).  The batches' streams, coded from a zero carry on their own
+    contexts and joined in order, must give the reference encoder's bytes; the chained multi-context
+    decode must give the Java-semantics decode."""
+    fr = pkg.synthetic.frames(w, h, frames, kind=kind)
+    n_stacks = (frames + 7) // 8
+    padded = np.zeros((n_stacks * 8, h, w), np.uint8)
+    padded[:frames] = fr
+    raw = tmp_path / "in.raw"
+    raw.write_bytes(fr.tobytes())
+    binf, outf = tmp_path / "out.bin", tmp_path / "out.raw"
+    env = dict(os.environ, DCT3D_CODEC_BATCH=batch)
+    r = subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), devices],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count("Frames processed") == n_stacks
+    q = plan8.encode_q(padded).reshape(-1)
+    assert binf.read_bytes() == reference_entropy_encode(q, w, h, n_stacks, 8)
+    r = subprocess.run([pkg.CLI_PATH, "decode", str(binf), str(outf), str(w), str(h), str(frames), devices],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    dec = np.frombuffer(outf.read_bytes(), np.uint8).reshape(n_stacks * 8, h, w)
+    assert np.array_equal(dec, plan8.decode_q(q.reshape(-1, 8, 8, 8), w, h, n_stacks * 8))
+
+
+def test_cli_multi_device_truncated_and_bad_device(pkg, tmp_path):
+    w, h, frames = 64, 48, 24
+    fr = pkg.synthetic.frames(w, h, frames, kind="uniform")
+    raw, binf, outf = tmp_path / "in.raw", tmp_path / "o.bin", tmp_path / "o.raw"
+    raw.write_bytes(fr.tobytes())
+    env = dict(os.environ, DCT3D_CODEC_BATCH="1")
+    assert subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), "1,1"],
+                          capture_output=True, env=env).returncode == 0
+    data = binf.read_bytes()
+    binf.write_bytes(data[: len(data) // 2])
+    r = subprocess.run([pkg.CLI_PATH, "decode", str(binf), str(outf), str(w), str(h), str(frames), "1,1"],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 1 and "Truncated or corrupt" in r.stdout
+    r = subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), "1,99"],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 1 and "device 99" in r.stdout
+
+
 def test_cli_depth4(pkg, plan4, tmp_path):
     w, h, frames = 64, 32, 8
     fr = pkg.synthetic.frames(w, h, frames, kind="uniform")
