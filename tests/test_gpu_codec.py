@@ -66,6 +66,30 @@ def test_cli_multi_device(pkg, plan8, tmp_path, w, h, frames, kind, devices, bat
     assert np.array_equal(dec, plan8.decode_q(q.reshape(-1, 8, 8, 8), w, h, n_stacks * 8))
 
 
+def test_cli_multi_device_depth4(pkg, plan4, tmp_path):
+    """encode_multi / decode_multi at block depth 4: the batches' streams joined behind the running partial
+    byte give the single-device .bin, and the chained decode the Java-semantics decode."""
+    w, h, frames = 64, 32, 20
+    fr = pkg.synthetic.frames(w, h, frames, kind="uniform")
+    n_stacks = (frames + 3) // 4
+    raw, b1, bm, outf = tmp_path / "in.raw", tmp_path / "one.bin", tmp_path / "multi.bin", tmp_path / "o.raw"
+    raw.write_bytes(fr.tobytes())
+    env = dict(os.environ, DCT3D_CODEC_BATCH="2")
+    for binf, dev in ((b1, "1"), (bm, "1,1,1")):
+        r = subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), dev, "4"],
+                           capture_output=True, text=True, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+    assert bm.read_bytes() == b1.read_bytes()
+    r = subprocess.run([pkg.CLI_PATH, "decode", str(bm), str(outf), str(w), str(h), str(frames), "1,1", "4"],
+                       capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    padded = np.zeros((n_stacks * 4, h, w), np.uint8)
+    padded[:frames] = fr
+    q = plan4.encode_q(padded)
+    dec = np.frombuffer(outf.read_bytes(), np.uint8).reshape(n_stacks * 4, h, w)
+    assert np.array_equal(dec, plan4.decode_q(q, w, h, n_stacks * 4))
+
+
 def test_cli_multi_device_truncated_and_bad_device(pkg, tmp_path):
     w, h, frames = 64, 48, 24
     fr = pkg.synthetic.frames(w, h, frames, kind="uniform")
