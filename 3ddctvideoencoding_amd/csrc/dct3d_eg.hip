@@ -475,10 +475,13 @@ __device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
 // short by avail takes no code; the next step continues it.  BOUNDED: room (>= 1) bits are left before
 // the parse's stop; the run ends there at the latest and a code is taken only if it starts before it,
 // so the parse ends exactly at the first code boundary at or past the stop (the code may reach past).
-template <bool BOUNDED = false>
-__device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& bad, uint32_t room = 32u) {
-    // ones at the top of hi, at most 31 (BOUNDED: at most room): the OR-ed bit makes clz defined and caps it
-    const uint32_t cap_bit = BOUNDED ? 0x80000000u >> min(room, 31u) : 1u;
+// CAP: the run's cap when unbounded (31; the mark pass's two-code step: 30, so that a step takes <= 32
+// values).  n1_out / w_out: the run's length and the code's width (0: none).
+template <bool BOUNDED = false, uint32_t CAP = 31u>
+__device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& bad, uint32_t room = 32u,
+                                              uint32_t* n1_out = nullptr, uint32_t* w_out = nullptr) {
+    // ones at the top of hi, at most CAP (BOUNDED: at most room): the OR-ed bit makes clz defined and caps it
+    const uint32_t cap_bit = BOUNDED ? 0x80000000u >> min(room, 31u) : 0x80000000u >> CAP;
     uint32_t n1 = __builtin_clz(~c.hi | cap_bit);
     uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
     c.avail -= n1;
@@ -503,7 +506,27 @@ __device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& 
     c.hi = (uint32_t)(b >> 32);
     c.lo = (uint32_t)b;
     c.avail -= w;
+    if (n1_out) *n1_out = n1;
+    if (w_out) *w_out = w;
     return n1 + (take ? 1u : 0u);
+}
+// lean_step, then a second code when it lies wholly in the buffered bits (no refill between): dense
+// content (few 1-bit codes, the steps mostly a run of 0-1 and one code) takes two codes per step.  A step
+// moves at most CAP + 31 + 31 bits and CAP + 2 values; the second code starts at bit n1 + w of the step.
+template <uint32_t CAP = 31u>
+__device__ __forceinline__ uint32_t lean_step2(const uint32_t* s, Lean& c, bool& bad, uint32_t* n1_out = nullptr,
+                                               uint32_t* w_out = nullptr) {
+    const uint32_t n = lean_step<false, CAP>(s, c, bad, 32u, n1_out, w_out);
+    // bits past avail are zero: a code whose leading zeros run past them is not taken (w2 > avail)
+    const uint32_t z2 = (uint32_t)__builtin_clz(c.hi | 1u);
+    const uint32_t w2 = 2u * z2 + 1u;
+    const bool take2 = !bad && z2 < 16u && w2 <= c.avail;
+    const uint32_t sh = take2 ? w2 : 0u;
+    const uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << sh;
+    c.hi = (uint32_t)(b >> 32);
+    c.lo = (uint32_t)b;
+    c.avail -= sh;
+    return n + (take2 ? 1u : 0u);
 }
 
 // The resolve walk of chunk t (pass 0 with resolve, below): e = the pass-0 exit of chunk t - 1 (~0u: it
@@ -590,7 +613,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
         const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
         Lean c = lean_from(r);
         bool bad = false;
-        while (!bad & (c.pos() < fast_stop)) n += lean_step(win, c, bad);
+        while (!bad & (c.pos() < fast_stop)) n += lean_step2(win, c, bad);
         while (!bad & (c.pos() < bstop)) n += lean_step<true>(win, c, bad, bstop - c.pos());
         lean_to(r, c);
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
@@ -674,9 +697,16 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
             myk[d0 < nv ? (ph + i + d0) / kMarkVals : kMkSlot - 1] = (uint16_t)(p0 + d0 - sp);  // no branch
             i += nv;
         };
+        // two-code steps (a run of <= 30, a code, a second code when buffered: nv <= 32): value i + d at bit
+        // p0 + d for d <= n1 (the run, then the first code), the second code at p0 + n1 + w
         while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
             const uint32_t p0 = c.pos();
-            mark(p0, lean_step(win, c, bad));
+            uint32_t n1, w;
+            const uint32_t nv = lean_step2<30u>(win, c, bad, &n1, &w);
+            const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
+            const uint32_t at = p0 + d0 + (d0 > n1 ? w - 1u : 0u);
+            myk[d0 < nv ? (ph + i + d0) / kMarkVals : kMkSlot - 1] = (uint16_t)(at - sp);  // no branch
+            i += nv;
         }
         // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
         // end take the checked steps)
