@@ -256,104 +256,70 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
     if (g + 1 == P.n_cubes || (end >> 5) != wl) P.out[wl] = P.tail[g];
 }
 
-// Fused path, K3: one wave per segment (8 cubes coded by encode_eg_kernel, lane l's words at rows
-// i*64 + eg_slot_col(l) of the slot; a lane-major slot measured K1 2.06 -> 2.21 ms and this kernel 0.28 -> 0.98 ms).  Lane l's bits go to stream bit off[s] + (bits of lanes < l): its words are
-// shifted into place; the word it shares with lane l + 1 is merged through a shuffle (every coding lane
-// has >= 32 bits, so a word has at most two contributors); the segment's first and last word go to
-// head / tail for eg_stitch_kernel, like a cube of eg_write_kernel.  The first kCompactPF rows are loaded
-// before any is used, the next kCompactPF while they are placed.  The interior words are placed in a
-// wave-private LDS image of the segment and leave as whole consecutive words, lane j storing words j,
-// j + 64, ... (round 4: stored straight from the lanes, each store instruction hit 64 scattered partial
-// lines); a segment longer than the image (never for 8-bit content) stores straight from the lanes.
-constexpr uint32_t kCompactImg = 1024;  // words per wave (a typical segment: ~180)
-constexpr int kCompactPF = 4;            // rows per load round trip (8: no gain)
+// Fused path, K3: kCompactSPW consecutive segments (8 cubes each, coded by encode_eg_kernel) per wave.
+// The slot holds a segment's stream, its first bit at bit 31 of word 0 (K1 places every lane's codes at
+// the lane's bit offset in the segment), so the segment's words only move to its stream offset off[s]:
+// output word i = slot words i - 1 and i funnel-shifted by off[s] mod 32, byte-swapped, lane j handling
+// words j, j + 64, ... (consecutive words per store instruction).  kCompactPF rows of 64 words of every
+// segment of the wave per load round trip (a segment of 1080p ramp content: ~180 words, uniform noise
+// ~420).  The first and the last word of a segment,
+// which it may share with its neighbours, go to head / tail for eg_stitch_kernel, like a cube of
+// eg_write_kernel.  (Round 4 before: lane-local words in slot columns and a lane bit-count array, the
+// lanes concatenated here through shuffles and an LDS image: 275 us per c7 step, 0.42 GB of slot reads;
+// one segment per wave: 201 us, two dependent round trips per 180 words.)
+constexpr int kCompactPF = 4;   // rows of 64 words per segment per load round trip
+constexpr int kCompactSPW = 4;  // segments per wave
 __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
-                                                              const uint16_t* __restrict__ lane_bits, uint32_t seg_cap) {
-    __shared__ uint32_t s_img[kEgWaves][kCompactImg];
+                                                              uint32_t seg_cap) {
     if (P.status[1] != 0) return;  // capacity failure: nothing is written
     const int lane = threadIdx.x & 63;
-    const uint64_t s = (uint64_t)blockIdx.x * kEgWaves + (threadIdx.x >> 6);
-    if (s >= P.n_cubes) return;
-    // wave-uniform (scalar) bases with 32-bit lane offsets: the segment's slot and its first output word
-    const uint32_t* seg = slot + (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)s) * seg_cap;
-    // independent loads, one round trip: the first rows unconditionally (a slot has >= 27 rows; words
-    // past a lane's last one are never used), its bit count, the segment offset
-    uint32_t buf[kCompactPF];
-    const uint32_t col = eg_slot_col((uint32_t)lane);
+    // wave-uniform (scalar) segment index, offsets and sizes; 32-bit lane offsets
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)((blockIdx.x * kEgWaves + (threadIdx.x >> 6)) * kCompactSPW));
+    if (s0 >= P.n_cubes) return;
+    uint64_t base[kCompactSPW];
+    uint32_t nsrc[kCompactSPW], ndst[kCompactSPW];
 #pragma unroll
-    for (int t = 0; t < kCompactPF; t++) buf[t] = seg[t * 64 + col];
-    const uint32_t lb = lane_bits[s * 64 + lane];
-    const uint64_t base = P.off[s];
-    uint32_t* const outs = P.out + (base >> 5);
-    const uint32_t nsrc = (lb + 31) >> 5;
-    uint32_t incl = lb;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
+    for (int t = 0; t < kCompactSPW; t++) {
+        const bool live = s0 + t < P.n_cubes;
+        base[t] = live ? P.off[s0 + t] : 0;
+        const uint32_t tot = live ? P.bits[s0 + t] : 0u;  // >= 256 for a live segment (a whole cube)
+        nsrc[t] = (tot + 31) >> 5;
+        ndst[t] = tot ? (uint32_t)(((base[t] + tot - 1) >> 5) - (base[t] >> 5) + 1) : 0u;
     }
-    const uint64_t start = base + (incl - lb);
-    const uint32_t r = (uint32_t)(start & 31);
-    const uint64_t w0 = start >> 5;
-    const uint32_t wrel = (uint32_t)(w0 - (base >> 5));  // < 54 * 64 words into the segment
-    const uint32_t ndst = lb ? (uint32_t)(((start + lb - 1) >> 5) - w0 + 1) : 0u;
-    const uint32_t nlb = __shfl_down(lb, 1, 64);
-    const bool next_shares = lane < 63 && nlb != 0u && ((start + lb) & 31) != 0;
-    const bool last_lane = lb != 0u && (lane == 63 || nlb == 0u);
-    // the segment's words relative to its first one (base >> 5): [0, nimg); 0 and nimg - 1 are head / tail
-    const uint32_t tot = __shfl(incl, 63, 64);
-    const uint32_t nimg = tot ? (uint32_t)(((base + tot - 1) >> 5) - (base >> 5) + 1) : 0u;
-    const bool staged = nimg <= kCompactImg;  // wave-uniform
-    uint32_t* const img = s_img[threadIdx.x >> 6];
-    auto put = [&](uint32_t rel, uint32_t v) {  // an interior word, rel in [1, nimg - 1)
-        if (staged) img[rel] = v;
-        else outs[rel] = v;
-    };
-    uint32_t prev = 0, first = 0, last = 0;
-    for (uint32_t d0 = 0; d0 < ndst; d0 += kCompactPF) {
-        // the next rows in flight while these are placed: a dense lane (the low-frequency part of a
-        // cube: up to 54 rows) waits one load round trip per kCompactPF rows, not per row
-        uint32_t nxt[kCompactPF];
+    auto load_rows = [&](int t, uint32_t i0, uint32_t (&cur)[kCompactPF], uint32_t (&prv)[kCompactPF]) {
+        const uint32_t* seg = slot + (uint64_t)(s0 + t) * seg_cap;
 #pragma unroll
-        for (int t = 0; t < kCompactPF; t++) {
-            const uint32_t d = d0 + kCompactPF + t;
-            nxt[t] = d < nsrc ? seg[d * 64u + col] : 0u;
+        for (int r = 0; r < kCompactPF; r++) {  // word i - 1: an L1 hit
+            const uint32_t i = i0 + r * 64 + lane;
+            cur[r] = i < nsrc[t] ? seg[i] : 0u;
+            prv[r] = i - 1u < nsrc[t] ? seg[i - 1u] : 0u;  // i = 0: none
         }
+    };
+    auto store_rows = [&](int t, uint32_t i0, const uint32_t (&cur)[kCompactPF], const uint32_t (&prv)[kCompactPF]) {
+        const uint32_t r = (uint32_t)(base[t] & 31);
+        uint32_t* const outs = P.out + (base[t] >> 5);
 #pragma unroll
-        for (int t = 0; t < kCompactPF; t++) {
-            const uint32_t d = d0 + t;
-            if (d < ndst) {
-                const uint32_t cur = d < nsrc ? buf[t] : 0u;
-                const uint32_t v = r ? ((cur >> r) | (prev << (32 - r))) : cur;
-                prev = cur;
-                if (d == 0) first = v;
-                if (d == ndst - 1) last = v;
-                if (d != 0 && d != ndst - 1) put(wrel + d, __builtin_bswap32(v));
+        for (int k = 0; k < kCompactPF; k++) {
+            const uint32_t i = i0 + k * 64 + lane;
+            if (i < ndst[t]) {
+                const uint32_t v = __builtin_bswap32(__builtin_amdgcn_alignbit(prv[k], cur[k], r));
+                if (i == 0) P.head[s0 + t] = v;
+                else if (i == ndst[t] - 1) P.tail[s0 + t] = v;
+                else outs[i] = v;
             }
         }
+    };
+    uint32_t nmax = 0;
 #pragma unroll
-        for (int t = 0; t < kCompactPF; t++) buf[t] = nxt[t];
+    for (int t = 0; t < kCompactSPW; t++) nmax = max(nmax, ndst[t]);
+    for (uint32_t i0 = 0; i0 < nmax; i0 += kCompactPF * 64) {  // all segments' rows in flight together
+        uint32_t cur[kCompactSPW][kCompactPF], prv[kCompactSPW][kCompactPF];
+#pragma unroll
+        for (int t = 0; t < kCompactSPW; t++) load_rows(t, i0, cur[t], prv[t]);
+#pragma unroll
+        for (int t = 0; t < kCompactSPW; t++) store_rows(t, i0, cur[t], prv[t]);
     }
-    const uint32_t nfirst = __shfl_down(first, 1, 64);
-    if (next_shares) last |= nfirst;  // ndst == 1 only when r == 0 and lb == 32: never shared then
-    if (ndst != 0) {
-        const bool shares_prev = lane > 0 && r != 0;  // my first word belongs to lane - 1's last store
-        if (ndst == 1) {
-            if (lane == 0) P.head[s] = __builtin_bswap32(first);
-            else if (last_lane) P.tail[s] = __builtin_bswap32(last);
-            else put(wrel, __builtin_bswap32(last));
-        } else {
-            if (lane == 0) P.head[s] = __builtin_bswap32(first);
-            else if (!shares_prev) put(wrel, __builtin_bswap32(first));
-            if (last_lane) P.tail[s] = __builtin_bswap32(last);
-            else put(wrel + ndst - 1, __builtin_bswap32(last));
-        }
-    }
-    if (!staged || nimg < 3) return;  // wave-uniform
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t i = 1 + (uint32_t)lane; i + 1 < nimg; i += 64) outs[i] = img[i];
 }
 
 // =================================================================================================
@@ -855,12 +821,12 @@ int launch_eg_scan(const EgParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,
-                      hipStream_t st) {
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     if (launch_eg_scan(P, st)) return -1;
-    const uint64_t blocks = (P.n_cubes + kEgWaves - 1) / kEgWaves;
-    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, lane_bits, seg_cap);
+    const uint64_t per = (uint64_t)kEgWaves * kCompactSPW;
+    const uint64_t blocks = (P.n_cubes + per - 1) / per;
+    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
     hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -111,21 +111,16 @@ struct EgDecParams {
 // Fused encode + Exp-Golomb (dct3d_encode_eg_dev): the encode kernel's transform / quantise /
 // certify, the exact Java replay of uncertified coefficients inside the wave, then the wave's 8
 // cubes coded straight into a private slot (no int32 cube-major round trip).  Segment = one wave = 8
-// consecutive cubes; lane l codes 1/8 of one cube's diagonal stream into its words of the slot.
-// Column of coding lane l = (cube c, part) in a slot row: part-major (part * 8 + c), so that the 8
-// low-frequency lanes (part 0, the most words) share one 32-byte piece of each row past the short
-// lanes' last word instead of touching four 64-byte lines of it.
-__host__ __device__ constexpr uint32_t eg_slot_col(uint32_t l) { return (l & 7u) * 8u + (l >> 3); }
+// consecutive cubes; lane l codes 1/8 of one cube's diagonal stream at its bit offset in the segment.
 
 struct EgFusedParams {
     const int32_t* ngroups;    // exact replay tables (as EncodeParams)
     const double* coef;
     const uint8_t* group_of;
     const uint16_t* diag;      // [cs] stream position -> cube index
-    uint32_t* slot;            // [n_seg * seg_cap]: word i of lane l at i*64 + eg_slot_col(l), MSB-first,
-                               // each lane's first bit at bit 31 of its word 0
+    uint32_t* slot;            // [n_seg * seg_cap]: the segment's stream, MSB-first words, its first bit
+                               // at bit 31 of word 0
     uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
-    uint16_t* lane_bits;       // [n_seg * 64] bits coded by each lane
     uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
 };
 
@@ -134,8 +129,7 @@ int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipSt
 int launch_eg_stitch(const EgParams& P, hipStream_t st);
 // scan of the segment bits + the lanes' words concatenated into the stream + stitch (P.n_cubes =
 // segments, P.bits = seg_bits)
-int launch_eg_compact(const EgParams& P, const uint32_t* slot, const uint16_t* lane_bits, uint32_t seg_cap,
-                      hipStream_t st);
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, hipStream_t st);
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 // resolve (pass 0): each chunk's true parse is followed from the exit of chunk t - 1 until it meets a
 // pass-0 boundary of chunk t (in the block's LDS window); status[0] = 0: every chunk met, the pass-0 exits

@@ -57,17 +57,22 @@ __device__ __forceinline__ uint64_t eg_push(uint64_t g, uint32_t w, uint32_t cod
 }
 
 // Append W < 64 stream bits (the low W bits of g, MSB first) to a lane's pending bits (p: the low nb <
-// 32 bits, nothing above them), branch-free.  The words completed (0, 1 or 2) go to the lane's next slot
-// rows through the segment's buffer descriptor (a lane without a word stores out of range: dropped);
-// the bits left pending are the low T mod 32 bits of p * 2^W + g.
+// 32 bits, nothing above them), branch-free.  The words completed (0, 1 or 2) go to the lane's next
+// words of the segment through its buffer descriptor (a lane without a word stores out of range:
+// dropped), except the lane's first word when it shares it with lane - 1 (dofs == hofs): that one is
+// kept in `head` for lane - 1's last store.  The bits left pending are the low T mod 32 bits of
+// p * 2^W + g.
 __device__ __forceinline__ void eg_append(uint64_t g, uint32_t W, uint32_t& p, uint32_t& nb,
-                                          __amdgpu_buffer_rsrc_t seg, uint32_t& dofs) {
+                                          __amdgpu_buffer_rsrc_t seg, uint32_t& dofs, uint32_t hofs,
+                                          uint32_t& head) {
     const uint32_t T = nb + W;
     const uint32_t w0 = (p << ((32u - nb) & 31u)) | (uint32_t)(g >> ((T - 32u) & 63u));
     const uint32_t w1 = (uint32_t)(g >> ((T - 64u) & 63u));
-    __builtin_amdgcn_raw_buffer_store_b32(w0, seg, (int)(T >= 32u ? dofs : 0x80000000u), 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b32(w1, seg, (int)(T >= 64u ? dofs + 256u : 0x80000000u), 0, 0);
-    dofs += (T >> 5) << 8;
+    const bool hd = dofs == hofs;
+    __builtin_amdgcn_raw_buffer_store_b32(w0, seg, (int)(T >= 32u && !hd ? dofs : 0x80000000u), 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w1, seg, (int)(T >= 64u ? dofs + 4u : 0x80000000u), 0, 0);
+    head = T >= 32u && hd ? w0 : head;
+    dofs += (T >> 5) << 2;
     p = __builtin_amdgcn_ubfe((uint32_t)((uint64_t)p << W) | (uint32_t)g, 0u, T & 31u);
     nb = T & 31u;
 }
@@ -195,54 +200,85 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
         }
     }
 
-    // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp, read from the
-    // staged codes 8 at a time: the 8 codes concatenated into one 64-bit group when they fit (W < 64;
-    // else one by one), each group appended to the lane's pending bits with at most two words out, word
-    // i of lane l at slot row i (i*64 + eg_slot_col(l)).  eg_compact_kernel concatenates the lanes.  (Buffering the
-    // words in LDS first needs the values in registers to free the region: +6 % kernel time for the pack
-    // / unpack, more than the scattered stores cost.)
+    // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp (lane order =
+    // stream order), read from the staged codes 8 at a time.  First the lane's bit count (the sum of its
+    // code widths, 63 - 2 clz each), the wave's exclusive scan of the counts: the lane's first bit in
+    // the segment.  Then the codes: 8 concatenated into one 64-bit group when they fit (W < 64; else one
+    // by one), each group appended to the lane's pending bits -- which start as the off mod 32 bits of
+    // the lanes before it, zeros here -- with at most two words out, at the segment's word index: the
+    // slot holds the segment's stream, and eg_compact_kernel only shifts it to the segment's offset.  A
+    // word two lanes share (every coding lane has >= VPL bits, so at most two) is stored once, by the
+    // first lane, merged with the second lane's part through a shuffle.  (Round 4 before: lane-local
+    // words in slot columns, concatenated by the compaction: 0.55 GB of partial-line slot stores and a
+    // lane bit-count array for a 0.37 GB stream.  Buffering the words in LDS needs the values in
+    // registers to free the region: +6 % kernel time for the pack / unpack.)
     const int cp = lane >> 3, part = lane & 7;
     const bool lvalid = cube0 + cp < P.n_cubes;
     const char* cb = wl + cp * CUBE_B;
+    uint32_t zs = 0;  // sum of the leading-zero counts of the lane's codes
+    uint32_t cds[VPL / 2];  // the lane's codes, two per register, kept for the emission
+    if (lvalid) {
+#pragma unroll
+        for (int i0 = 0; i0 < VPL; i0 += 8) {
+            const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
+            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+                const uint32_t lo = *(const uint16_t*)(cb + (pw[e >> 1] & 0xFFFFu));
+                const uint32_t hi = *(const uint16_t*)(cb + (pw[e >> 1] >> 16));
+                cds[(i0 + e) / 2] = lo | (hi << 16);
+                zs += __builtin_clz(lo) + __builtin_clz(hi);
+            }
+        }
+    }
+    const uint32_t lbits = lvalid ? 63u * VPL - 2u * zs : 0u;
+    uint32_t incl = lbits;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+    }
+    const uint32_t off = incl - lbits;  // the lane's first bit in the segment
     // the segment's slot (wave-uniform base and size) as a buffer descriptor; each store adds a 32-bit
     // lane offset
     const __amdgpu_buffer_rsrc_t seg = __builtin_amdgcn_make_buffer_rsrc(
         E.slot + (size_t)__builtin_amdgcn_readfirstlane(wid) * E.seg_cap, (short)0, (int)(E.seg_cap * 4u), 0x00020000);
-    const uint32_t col4 = eg_slot_col((uint32_t)lane) * 4u;
-    uint32_t dofs = col4;  // byte offset of the lane's next word: (nw * 64 + col) * 4
-    uint32_t p = 0, nb = 0;
+    uint32_t dofs = (off >> 5) * 4u;  // byte offset of the lane's next word in the segment
+    const uint32_t hofs = (off & 31u) ? dofs : 0xFFFFFFFFu;  // its first word, when shared with lane - 1
+    uint32_t p = 0, nb = lvalid ? (off & 31u) : 0u, head = 0;
     if (lvalid) {
-#pragma unroll 1
+#pragma unroll
         for (int i0 = 0; i0 < VPL; i0 += 8) {
-            const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
-            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
             uint32_t cd[8], w[8];
 #pragma unroll
-            for (int e = 0; e < 8; e++) cd[e] = *(const uint16_t*)(cb + ((pw[e >> 1] >> (16 * (e & 1))) & 0xFFFFu));
-            uint64_t g = 0;
-            uint32_t W = 0;
+            for (int e = 0; e < 8; e++) cd[e] = (e & 1) ? cds[(i0 + e) / 2] >> 16 : cds[(i0 + e) / 2] & 0xFFFFu;
+            // group 0 (the DC and the lowest frequencies: > 64 bits in every wave of 1080p ramp and uniform
+            // content, <= 64 bits per half in all of them) as two halves of 4 codes; the others as one
+            // group of 8 (> 64 bits in 2 % of the waves at group 1 on uniform content, never later)
+            constexpr int NH = 2;
+            uint64_t g[NH] = {0, 0};
+            uint32_t W[NH] = {0, 0};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 w[e] = eg_width(cd[e]);
-                g = eg_push(g, w[e], cd[e]);
-                W += w[e];
+                const int h = i0 == 0 ? e / 4 : 0;
+                g[h] = eg_push(g[h], w[e], cd[e]);
+                W[h] += w[e];
             }
-            if (__builtin_expect(W < 64u, 1)) {
-                eg_append(g, W, p, nb, seg, dofs);
+            if (__builtin_expect(W[0] < 64u && W[1] < 64u, 1)) {
+                eg_append(g[0], W[0], p, nb, seg, dofs, hofs, head);
+                if (i0 == 0) eg_append(g[1], W[1], p, nb, seg, dofs, hofs, head);
             } else {
 #pragma unroll
-                for (int e = 0; e < 8; e++) eg_append(cd[e], w[e], p, nb, seg, dofs);
+                for (int e = 0; e < 8; e++) eg_append(cd[e], w[e], p, nb, seg, dofs, hofs, head);
             }
         }
-        __builtin_amdgcn_raw_buffer_store_b32(p << ((32u - nb) & 31u), seg, (int)(nb ? dofs : 0x80000000u), 0, 0);
     }
-    const uint32_t nw = (dofs - col4) >> 8;  // full words stored
-    const uint32_t lbits = lvalid ? nw * 32u + nb : 0u;
-    E.lane_bits[(size_t)wid * 64 + lane] = (uint16_t)lbits;
-    uint32_t tot = lbits;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-    if (lane == 0) E.seg_bits[wid] = tot;
+    // the lane's last, partial word, completed by lane + 1's first bits (lane + 1 starts inside it)
+    const uint32_t nh = __shfl_down(head, 1, 64);
+    __builtin_amdgcn_raw_buffer_store_b32((p << ((32u - nb) & 31u)) | (lane < 63 ? nh : 0u), seg,
+                                          (int)(nb ? dofs : 0x80000000u), 0, 0);
+    if (lane == 63) E.seg_bits[wid] = incl;
 }
 
 

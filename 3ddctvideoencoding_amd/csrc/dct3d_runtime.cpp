@@ -87,7 +87,7 @@ struct dct3d_ctx {
     // Exp-Golomb stage: diagonal order, per-cube bits / offsets, chunk sums, status, device stream
     DevBuf d_diag, d_eg_bits, d_eg_off, d_eg_bsum, d_eg_status, d_eg_out, d_eg_q, d_eg_ht;
     // fused encode + Exp-Golomb: per-segment slots and lane bit counts
-    DevBuf d_egf_slot, d_egf_lbits;
+    DevBuf d_egf_slot;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
@@ -247,8 +247,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
                       &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egd_mark,
-                      &c->d_egf_slot,
-                      &c->d_egf_lbits})
+                      &c->d_egf_slot})
         b->release();
     for (auto& q : c->ev)
         for (auto& e : q)
@@ -824,7 +823,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     // two passes: K1 codes into per-segment slots, then scan + compaction (a single pass by decoupled
     // look-back wrote the same stream but measured slower: DESIGN.md §4b)
     if ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
-        (rc = c->d_egf_lbits.grow(n_seg * 64 * sizeof(uint16_t))) || (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
+        (rc = c->d_eg_bits.grow(n_seg * sizeof(uint32_t))) ||
         (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
         (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
         return rc;
@@ -853,7 +852,6 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     E.diag = (const uint16_t*)c->d_diag.p;
     E.slot = (uint32_t*)c->d_egf_slot.p;
     E.seg_cap = seg_cap;
-    E.lane_bits = (uint16_t*)c->d_egf_lbits.p;
     E.seg_bits = (uint32_t*)c->d_eg_bits.p;
     EgParams G;
     G.q = nullptr;
@@ -875,7 +873,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (launch_encode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
-    if (launch_eg_compact(G, E.slot, E.lane_bits, seg_cap, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_compact(G, E.slot, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)

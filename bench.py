@@ -571,8 +571,8 @@ def main():
     if direction in ("forward_f32", "inverse_f32"):
         bytes_per_cube = cs * (4 + 4)  # f32 in + f32 out (4,096 B per cube)
     fused = direction == "encode_eg" and not a.eg_two_step
-    if fused:  # u8 in + the cube's share of the coded stream, lane bit counts and segment totals out
-        bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes) + (64 * 2 + 4) / 8
+    if fused:  # u8 in + the cube's share of the coded stream and of the segment bit totals out
+        bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes) + 4 / 8
     fused_dec = direction == "decode_eg" and not a.eg_two_step
     if fused_dec:  # the cube's share of the stream in, u8 out
         bytes_per_cube = cs + eg_info["bits"] / 8 / max(1, n_cubes)

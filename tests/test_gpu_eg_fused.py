@@ -37,11 +37,17 @@ def _content(pkg, kind, w, h, f):
     if kind == "checker":   # extreme AC coefficients (largest codes)
         z, y, x = np.indices((f, h, w))
         return (((x + y + z) & 1) * 255).astype(np.uint8)
+    if kind == "corner":    # a large DC and first-order coefficients: group 0's halves > 64 bits
+        z, y, x = np.indices((f, h, w))
+        return np.where((x % 8) + (y % 8) + (z % 8) < 10, 255, 0).astype(np.uint8)
+    if kind == "edge":      # group 0's halves of exactly 64 bits at 8x8x4
+        z, y, x = np.indices((f, h, w))
+        return np.where((x % 8) + (y % 8) + (z % 4) < 5, 255, 0).astype(np.uint8)
     raise ValueError(kind)
 
 
 @pytest.mark.parametrize("depth", [8, 4])
-@pytest.mark.parametrize("kind", ["ramp", "uniform", "zeros", "full", "checker"])
+@pytest.mark.parametrize("kind", ["ramp", "uniform", "zeros", "full", "checker", "corner", "edge"])
 def test_fused_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, kind):
     ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
     fr = _content(pkg, kind, 64, 64, 2 * depth)
