@@ -735,9 +735,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const uint64_t last = m0 + 64 < n_marks ? P.mark[m0 + 64] : P.status[1];  // wave-uniform
     const uint64_t w0 = first >> 5;
     const uint64_t span = (last >> 5) + 4 - w0;
-    const bool fits = span <= kEmitWinWords;  // wave-uniform
+    const bool fits = span <= kEmitWinWords - 1;  // wave-uniform
     const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* wl = lds[wave];
+    uint32_t* win = wl + 1;  // the window one word into the region: parse_pairs reads win[-1]
     // 4 loads in flight per lane before the LDS writes (as decode_eg_kernel's staging)
     const uint32_t nst = P.n_words ? nwin : 0u;  // (an empty stream: reported by the mark pass)
     for (uint32_t i0 = 0; i0 < nst; i0 += 256) {
@@ -747,14 +748,14 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
 #pragma unroll
         for (int b = 0; b < 4; b++) {
             const uint32_t i = i0 + b * 64 + lane;
-            if (i < nwin) wl[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
+            if (i < nwin) win[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int32_t v[kMarkVals];
-    parse_values<kMarkVals>(P, wl, nwin, w0, fits, my, v);
+    parse_values<kMarkVals>(P, win, nwin, w0, fits, my, v);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

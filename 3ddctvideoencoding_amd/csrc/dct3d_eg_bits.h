@@ -231,8 +231,60 @@ __device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader
     return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
 }
 
+// 31 - 2 z (32 - the width of a code with z leading zeros) as one v_mad_i32_i24 (the compiler would emit
+// a shift and a subtract)
+__device__ __forceinline__ uint32_t eg_rshift(uint32_t z) {
+    uint32_t r;
+    asm("v_mad_i32_i24 %0, %1, -2, 31" : "=v"(r) : "v"(z));
+    return r;
+}
+
+// The code at window bit q (any valid width, up to 63 bits): the rare long code of parse_pairs
+__device__ __forceinline__ uint32_t win_code_at(const uint32_t* win, uint32_t& q) {
+    const uint32_t k = q >> 5, sh = q & 31u;
+    const uint64_t h = (((uint64_t)win[k] << 32) | win[k + 1]) << sh;
+    const uint64_t x = sh ? (h | (win[k + 2] >> (32u - sh))) : h;
+    const uint32_t w = 2u * (uint32_t)__builtin_clzll(x) + 1u;  // a validated stream: < 32 leading zeros
+    q += w;
+    return (uint32_t)(x >> (64u - w));
+}
+
+// A consumer lane's N values from window bit p of a validated stream, two codes per step read from
+// the window itself: words k - 1, k, k + 1 (k = ceil(p / 32)) funnel-shifted by p mod 32 hold the 64
+// bits at p, and two codes of <= 31 bits (|v| < 2^15: every code an encoder of 8-bit frames writes)
+// take at most 62 of them.  No buffer is carried between steps, so no refill test and no divergent
+// refill branch: a step is one LDS read pair, two funnel shifts per code pair and the two codes'
+// leading-zero counts, shifts and position update.  A longer code (wave-uniform test) re-reads both
+// codes at their absolute positions.  win[-1] must be readable (the window starts one word into its
+// region): it is read, and ignored, at p = 0.
+template <int N>
+__device__ __forceinline__ void parse_pairs(const uint32_t* win, uint32_t p, int32_t (&v)[N]) {
+    static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+    for (int i = 0; i < N; i += 2) {
+        const uint32_t* w = win + ((p + 31u) >> 5);
+        const uint32_t s = 0u - p;  // the funnel shift's low 5 bits: (32 - p mod 32) mod 32
+        const uint32_t a = w[-1], b = w[0], c = w[1];
+        const uint32_t hi = __builtin_amdgcn_alignbit(a, b, s);
+        const uint32_t lo = __builtin_amdgcn_alignbit(b, c, s);
+        const uint32_t s1 = eg_rshift(__builtin_clz(hi));  // 32 - width of the first code
+        const uint32_t h2 = __builtin_amdgcn_alignbit(hi, lo, s1);
+        const uint32_t s2 = eg_rshift(__builtin_clz(h2));
+        uint32_t c1 = hi >> s1, c2 = h2 >> s2;
+        if (__builtin_expect(__ballot(min(hi, h2) < 0x10000u) != 0ull, 0)) {  // a code of 33+ bits
+            c1 = win_code_at(win, p);
+            c2 = win_code_at(win, p);
+        } else {
+            p += 64u - (s1 + s2);
+        }
+        v[i] = eg_value_fast(c1);
+        v[i + 1] = eg_value_fast(c2);
+    }
+}
+
 // A consumer lane's N values from stream bit `my` (a mark: the stream is validated by the mark pass).
-// fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin)); else
+// fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin), win[-1]
+// readable: parse_pairs); else
 // the parse reads the stream in global memory -- a wave whose 2,048 values average more than the window
 // holds (|q| >= 2^13 nearly everywhere: never written by an encoder of 8-bit frames, but a valid stream).
 // That path's values pass through the (then unused) window region, lane-private rows of N words (64 N
@@ -242,12 +294,9 @@ template <int N>
 __device__ __forceinline__ void parse_values(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
                                              bool fits, uint64_t my, int32_t (&v)[N]) {
     if (fits) {
-        ValidWinReader r{win, nullptr, 0, 0, 0, 0};
-        r.seek(my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u);
-#pragma unroll
-        for (int i = 0; i < N; i++) v[i] = eg_value_fast(r.get());
+        parse_pairs<N>(win, my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u, v);
     } else {
-        int32_t* row = (int32_t*)win + (threadIdx.x & 63) * N;
+        int32_t* row = (int32_t*)(win - 1) + (threadIdx.x & 63) * N;  // from the region's first word
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
         r.seek(my);
         for (int i = 0; i < N; i++) {

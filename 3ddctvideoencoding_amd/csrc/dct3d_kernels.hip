@@ -463,7 +463,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     using G = DecGeom<D>;
     constexpr uint32_t CS = G::CS, PARTS = CS / 32, CPW = G::CPW;
     static_assert(CPW * CS == 2048 && PARTS * CPW == 64, "one wave = 64 marks");
-    constexpr uint32_t WIN = kDecWaveLds / 4;  // 2,320 words >= 2,048 values x 27 bits
+    constexpr uint32_t WIN = kDecWaveLds / 4 - 1;  // 2,319 words >= 2,048 values x 27 bits (+ win[-1])
     constexpr int NWP = 4;                     // window words per lane loaded ahead (256: 4 bits per value)
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kDecWaveLds];
     __shared__ uint16_t s_diag[CS];
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     __syncthreads();
     const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    uint32_t* win = (uint32_t*)wl;
+    uint32_t* win = (uint32_t*)wl + 1;  // the window one word into the region: parse_pairs reads win[-1]
     const uint64_t n_marks = E.n_values / 32;
     const uint32_t row0 = xcd_tile() * NG;  // the block's first round of 4 groups
     auto cube_of = [&](int i) { return P.cube_base + ((row0 + (uint32_t)i) * kWavesPerBlock + wave) * CPW; };
