@@ -738,7 +738,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const bool fits = span <= kEmitWinWords - 1;  // wave-uniform
     const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* wl = lds[wave];
-    uint32_t* win = wl + 1;  // the window one word into the region: parse_pairs reads win[-1]
+    uint32_t* win = wl + 1;  // the window one word into the region: parse_step reads win[-1]
     // 4 loads in flight per lane before the LDS writes (as decode_eg_kernel's staging)
     const uint32_t nst = P.n_words ? nwin : 0u;  // (an empty stream: reported by the mark pass)
     for (uint32_t i0 = 0; i0 < nst; i0 += 256) {

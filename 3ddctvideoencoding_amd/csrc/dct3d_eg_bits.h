@@ -239,7 +239,7 @@ __device__ __forceinline__ uint32_t eg_rshift(uint32_t z) {
     return r;
 }
 
-// The code at window bit q (any valid width, up to 63 bits): the rare long code of parse_pairs
+// The code at window bit q (any valid width, up to 63 bits): the rare long code of parse_step
 __device__ __forceinline__ uint32_t win_code_at(const uint32_t* win, uint32_t& q) {
     const uint32_t k = q >> 5, sh = q & 31u;
     const uint64_t h = (((uint64_t)win[k] << 32) | win[k + 1]) << sh;
@@ -249,42 +249,61 @@ __device__ __forceinline__ uint32_t win_code_at(const uint32_t* win, uint32_t& q
     return (uint32_t)(x >> (64u - w));
 }
 
-// A consumer lane's N values from window bit p of a validated stream, two codes per step read from
-// the window itself: words k - 1, k, k + 1 (k = ceil(p / 32)) funnel-shifted by p mod 32 hold the 64
-// bits at p, and two codes of <= 31 bits (|v| < 2^15: every code an encoder of 8-bit frames writes)
-// take at most 62 of them.  No buffer is carried between steps, so no refill test and no divergent
-// refill branch: a step is one LDS read pair, two funnel shifts per code pair and the two codes'
-// leading-zero counts, shifts and position update.  A longer code (wave-uniform test) re-reads both
-// codes at their absolute positions.  win[-1] must be readable (the window starts one word into its
-// region): it is read, and ignored, at p = 0.
-template <int N>
-__device__ __forceinline__ void parse_pairs(const uint32_t* win, uint32_t p, int32_t (&v)[N]) {
-    static_assert(N % 2 == 0, "pairs");
+// One parse step of a validated stream in an LDS window: C codes from window bit p, read from the window
+// itself.  Words k - 1 .. k + C - 1 (k = ceil(p / 32)) funnel-shifted by p mod 32 hold the 32 C bits at p,
+// and C codes of <= 31 bits (|v| < 2^15: every code an encoder of 8-bit frames writes) take at most 31 C
+// of them.  No buffer is carried between steps, so no refill test and no divergent refill branch: a step
+// is one round of LDS reads, C funnel shifts, and per code a leading-zero count, a shift and the funnel
+// shifts of the bits behind it.  A longer code (wave-uniform test) re-reads the step's codes at their
+// positions.  win[-1] must be readable (the window starts one word into its region): it is read, and
+// ignored, at p = 0.
+template <int C>
+__device__ __forceinline__ void parse_step(const uint32_t* win, uint32_t& p, uint32_t (&code)[C]) {
+    const uint32_t* w = win + ((p + 31u) >> 5);
+    const uint32_t s = 0u - p;  // the funnel shift's low 5 bits: (32 - p mod 32) mod 32
+    uint32_t x[C + 1], b[C], sh[C];
 #pragma unroll
-    for (int i = 0; i < N; i += 2) {
-        const uint32_t* w = win + ((p + 31u) >> 5);
-        const uint32_t s = 0u - p;  // the funnel shift's low 5 bits: (32 - p mod 32) mod 32
-        const uint32_t a = w[-1], b = w[0], c = w[1];
-        const uint32_t hi = __builtin_amdgcn_alignbit(a, b, s);
-        const uint32_t lo = __builtin_amdgcn_alignbit(b, c, s);
-        const uint32_t s1 = eg_rshift(__builtin_clz(hi));  // 32 - width of the first code
-        const uint32_t h2 = __builtin_amdgcn_alignbit(hi, lo, s1);
-        const uint32_t s2 = eg_rshift(__builtin_clz(h2));
-        uint32_t c1 = hi >> s1, c2 = h2 >> s2;
-        if (__builtin_expect(__ballot(min(hi, h2) < 0x10000u) != 0ull, 0)) {  // a code of 33+ bits
-            c1 = win_code_at(win, p);
-            c2 = win_code_at(win, p);
-        } else {
-            p += 64u - (s1 + s2);
-        }
-        v[i] = eg_value_fast(c1);
-        v[i + 1] = eg_value_fast(c2);
+    for (int j = 0; j <= C; j++) x[j] = w[j - 1];
+#pragma unroll
+    for (int j = 0; j < C; j++) b[j] = __builtin_amdgcn_alignbit(x[j], x[j + 1], s);
+    uint32_t mn = 0xFFFFFFFFu, sum = 0;
+#pragma unroll
+    for (int e = 0; e < C; e++) {
+        sh[e] = eg_rshift(__builtin_clz(b[0]));  // 32 - the code's width
+        code[e] = b[0] >> sh[e];
+        mn = min(mn, b[0]);
+        sum += sh[e];
+#pragma unroll
+        for (int j = 0; j + 1 < C - e; j++) b[j] = __builtin_amdgcn_alignbit(b[j], b[j + 1], sh[e]);
     }
+    if (__builtin_expect(__ballot(mn < 0x10000u) != 0ull, 0)) {  // a code of 33+ bits
+#pragma unroll
+        for (int e = 0; e < C; e++) code[e] = win_code_at(win, p);
+    } else {
+        p += 32u * C - sum;
+    }
+}
+
+// A consumer lane's N values from window bit p: three codes per step, a last step of two
+template <int N>
+__device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, int32_t (&v)[N]) {
+    static_assert(N >= 2 && (N - 2) % 3 == 0, "steps of three and a last one of two");
+#pragma unroll
+    for (int i = 0; i + 2 < N; i += 3) {
+        uint32_t c[3];
+        parse_step<3>(win, p, c);
+#pragma unroll
+        for (int e = 0; e < 3; e++) v[i + e] = eg_value_fast(c[e]);
+    }
+    uint32_t c[2];
+    parse_step<2>(win, p, c);
+    v[N - 2] = eg_value_fast(c[0]);
+    v[N - 1] = eg_value_fast(c[1]);
 }
 
 // A consumer lane's N values from stream bit `my` (a mark: the stream is validated by the mark pass).
 // fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin), win[-1]
-// readable: parse_pairs); else
+// readable: parse_step); else
 // the parse reads the stream in global memory -- a wave whose 2,048 values average more than the window
 // holds (|q| >= 2^13 nearly everywhere: never written by an encoder of 8-bit frames, but a valid stream).
 // That path's values pass through the (then unused) window region, lane-private rows of N words (64 N
@@ -294,7 +313,7 @@ template <int N>
 __device__ __forceinline__ void parse_values(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
                                              bool fits, uint64_t my, int32_t (&v)[N]) {
     if (fits) {
-        parse_pairs<N>(win, my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u, v);
+        parse_win<N>(win, my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u, v);
     } else {
         int32_t* row = (int32_t*)(win - 1) + (threadIdx.x & 63) * N;  // from the region's first word
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};

@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     __syncthreads();
     const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
     char* wl = lds + wave * kDecWaveLds;
-    uint32_t* win = (uint32_t*)wl + 1;  // the window one word into the region: parse_pairs reads win[-1]
+    uint32_t* win = (uint32_t*)wl + 1;  // the window one word into the region: parse_step reads win[-1]
     const uint64_t n_marks = E.n_values / 32;
     const uint32_t row0 = xcd_tile() * NG;  // the block's first round of 4 groups
     auto cube_of = [&](int i) { return P.cube_base + ((row0 + (uint32_t)i) * kWavesPerBlock + wave) * CPW; };
