@@ -5,6 +5,7 @@
 # for the per-kernel split.
 #   BASE=base OUT=r04_c7ab ROUNDS=3 UNIFORM=1 tools/gpu_build_ab.sh
 #   CONFIG=c8_decode_eg_1080p TESTS="tests/test_gpu_eg.py tests/test_gpu_eg_fused.py" tools/gpu_build_ab.sh
+# NEW=<name>: the "new" side from ab/<name> instead of the working tree (the tests still run here).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${OUT:-buildab}; B=${BASE:-base}; CFG=${CONFIG:-c7_encode_eg_1080p}; TAG=${CFG%%_*}
@@ -19,7 +20,7 @@ kinds="ramp"; [ -n "$UNIFORM" ] && kinds="ramp uniform"
 for i in $(seq 1 ${ROUNDS:-3}); do
   for kind in $kinds; do
     for side in $B new; do
-      dir=$ROOT; [ $side != new ] && dir=$ROOT/ab/$side
+      dir=$ROOT; [ $side != new ] && dir=$ROOT/ab/$side; [ $side = new ] && [ -n "$NEW" ] && dir=$ROOT/ab/$NEW
       (cd $dir && timeout -k 10 200 python bench.py --config $CFG --kind $kind --steps 20 --warmup 5 \
          --no-cpu-baseline --no-ceiling) > $O/${side}_${kind}_$i.log 2>&1
       rc=$?; [ $rc -ne 0 ] && { tail -5 $O/${side}_${kind}_$i.log; echo "stopping: $side rc=$rc"; exit $rc; }
@@ -29,7 +30,7 @@ for i in $(seq 1 ${ROUNDS:-3}); do
 done
 [ -n "$NO_PROF" ] && exit 0
 for side in $B new; do
-  dir=$ROOT; [ $side != new ] && dir=$ROOT/ab/$side
+  dir=$ROOT; [ $side != new ] && dir=$ROOT/ab/$side; [ $side = new ] && [ -n "$NEW" ] && dir=$ROOT/ab/$NEW
   (cd $dir && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $ROOT/$O/prof_$side -o run --output-format csv -- \
      python3 bench.py --config $CFG --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling) \
      > $O/prof_$side.log 2>&1 || { echo "rocprof $side failed"; tail -3 $O/prof_$side.log; exit 1; }
