@@ -56,6 +56,31 @@ __device__ __forceinline__ uint64_t eg_push(uint64_t g, uint32_t w, uint32_t cod
     return ((uint64_t)(uint32_t)(t >> 32) << 32) | (uint32_t)((uint32_t)t | code);
 }
 
+// The same on a code held in 16-bit half H of a register (two codes per register): SDWA operand
+// selects, so that the half is never unpacked (v_ffbh_u32 of the zero-extended half; v_or_b32 of it)
+template <int H>
+__device__ __forceinline__ uint32_t eg_width16(uint32_t x) {
+    uint32_t z, w;
+    if constexpr (H == 0)
+        asm("v_ffbh_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(z) : "v"(x));
+    else
+        asm("v_ffbh_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(z) : "v"(x));
+    asm("v_mad_i32_i24 %0, %1, -2, 63" : "=v"(w) : "v"(z));
+    return w;
+}
+template <int H>
+__device__ __forceinline__ uint64_t eg_push16(uint64_t g, uint32_t w, uint32_t x) {
+    const uint64_t t = g << (w & 63u);
+    uint32_t lo;
+    if constexpr (H == 0)
+        asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+            : "=v"(lo) : "v"((uint32_t)t), "v"(x));
+    else
+        asm("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+            : "=v"(lo) : "v"((uint32_t)t), "v"(x));
+    return ((uint64_t)(uint32_t)(t >> 32) << 32) | lo;
+}
+
 // Append W < 64 stream bits (the low W bits of g, MSB first) to a lane's pending bits (p: the low nb <
 // 32 bits, nothing above them), branch-free.  The words completed (0, 1 or 2) go to the lane's next
 // words of the segment through its buffer descriptor (a lane without a word stores out of range:
@@ -260,9 +285,10 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
             uint32_t W[NH] = {0, 0};
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                w[e] = eg_width(cd[e]);
+                const uint32_t x = cds[(i0 + e) / 2];
+                w[e] = (e & 1) ? eg_width16<1>(x) : eg_width16<0>(x);
                 const int h = i0 == 0 ? e / 4 : 0;
-                g[h] = eg_push(g[h], w[e], cd[e]);
+                g[h] = (e & 1) ? eg_push16<1>(g[h], w[e], x) : eg_push16<0>(g[h], w[e], x);
                 W[h] += w[e];
             }
             if (__builtin_expect(W[0] < 64u && W[1] < 64u, 1)) {
