@@ -147,7 +147,7 @@ struct WinReader {
         if (hi32 == 0u) return false;  // 32 zero bits: invalid
         const int width = 2 * __builtin_clz(hi32) + 1;
         const bool fits = width <= avail;
-        // the common case without a divergent if / else (as ValidWinReader)
+        // the common case without a divergent if / else
         code = (uint32_t)(buf >> (64 - width));
         buf <<= width;
         avail -= width;
@@ -164,58 +164,6 @@ struct WinReader {
             }
         }
         return true;
-    }
-};
-
-// A validated stream in an LDS window (the consumers after the mark pass): no bounds checks (a valid
-// parse stays inside the staged range, which carries 4 words of slack).  The buffer is two 32-bit words
-// hi:lo, left-aligned, its top `avail` bits valid and the rest zero; the position is implied
-// (next * 32 - avail), so a code costs a leading-zero count, one funnel shift (v_alignbit_b32) and one
-// shift instead of the 64-bit shifts and position update of a 64-bit buffer.  A refill appends the word
-// `pre` whenever fewer than 32 bits are buffered, so a code of up to 31 bits (|v| < 2^15: every code an
-// encoder of 8-bit frames writes) is always whole in hi:lo; a longer one is re-read at its absolute
-// position after a wave-uniform test.
-struct ValidWinReader {
-    const uint32_t* s;
-    const uint32_t* np;  // the word held in `pre` (a pointer, not an index: one add per refill, no address
-                         // arithmetic); the buffer ends at bit (np - s) * 32
-    uint32_t hi, lo;
-    uint32_t avail;
-    uint32_t pre;
-    __device__ __forceinline__ void seek(uint32_t p) {
-        const uint32_t k = p >> 5;
-        const uint64_t b = (((uint64_t)s[k] << 32) | s[k + 1]) << (p & 31);
-        hi = (uint32_t)(b >> 32);
-        lo = (uint32_t)b;
-        avail = 64u - (p & 31);
-        np = s + k + 2;
-        pre = *np;
-    }
-    __device__ __forceinline__ uint32_t get() {
-        if (avail < 32u) {  // hi holds the avail valid bits, lo is zero: pre goes right behind them
-            hi |= pre >> avail;
-            lo = __builtin_amdgcn_alignbit(pre, 0u, avail);  // pre << (32 - avail); 0 for avail = 0
-            avail += 32u;
-            pre = *++np;
-        }
-        const uint32_t z = __builtin_clz(hi);  // a valid code: hi (>= 32 buffered bits) is not 0
-        const uint32_t w = 2u * z + 1u;
-        uint32_t code = hi >> (32u - w);  // w <= 31 (z < 16); else garbage, replaced below
-        hi = __builtin_amdgcn_alignbit(hi, lo, 32u - w);
-        lo <<= w;
-        avail -= w;
-        if (__builtin_expect(__ballot(z >= 16u) != 0ull, 0)) {
-            if (z >= 16u) {  // a code of 33+ bits: read at its absolute position
-                const uint32_t p = (uint32_t)(np - s) * 32u - (avail + w);
-                const uint32_t k = p >> 5;
-                const int sh = (int)(p & 31);
-                const uint64_t h = (((uint64_t)s[k] << 32) | s[k + 1]) << sh;
-                const uint64_t x = sh ? (h | ((uint64_t)s[k + 2] >> (32 - sh))) : h;
-                code = (uint32_t)(x >> (64 - w));
-                seek(p + w);
-            }
-        }
-        return code;
     }
 };
 
