@@ -734,7 +734,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const uint64_t first = __shfl(my, 0, 64);
     const uint64_t last = m0 + 64 < n_marks ? P.mark[m0 + 64] : P.status[1];  // wave-uniform
     const uint64_t w0 = first >> 5;
-    const uint64_t span = (last >> 5) + 4 - w0;
+    const uint64_t span = (last >> 5) + 5 - w0;  // + 5 words of slack: parse_win
     const bool fits = span <= kEmitWinWords - 1;  // wave-uniform
     const uint32_t nwin = (uint32_t)(fits ? span : 0);
     uint32_t* wl = lds[wave];

@@ -232,21 +232,18 @@ __device__ __forceinline__ void parse_step(const uint32_t* win, uint32_t& p, uin
     }
 }
 
-// A consumer lane's N values from window bit p: three codes per step, a last step of two
+// A consumer lane's N values from window bit p: four codes per step (the window carries 5 words of slack
+// past the last mark: a step reads up to word ceil(p / 32) + 3)
 template <int N>
 __device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, int32_t (&v)[N]) {
-    static_assert(N >= 2 && (N - 2) % 3 == 0, "steps of three and a last one of two");
+    static_assert(N % 4 == 0, "steps of four");
 #pragma unroll
-    for (int i = 0; i + 2 < N; i += 3) {
-        uint32_t c[3];
-        parse_step<3>(win, p, c);
+    for (int i = 0; i < N; i += 4) {
+        uint32_t c[4];
+        parse_step<4>(win, p, c);
 #pragma unroll
-        for (int e = 0; e < 3; e++) v[i + e] = eg_value_fast(c[e]);
+        for (int e = 0; e < 4; e++) v[i + e] = eg_value_fast(c[e]);
     }
-    uint32_t c[2];
-    parse_step<2>(win, p, c);
-    v[N - 2] = eg_value_fast(c[0]);
-    v[N - 1] = eg_value_fast(c[1]);
 }
 
 // A consumer lane's N values from stream bit `my` (a mark: the stream is validated by the mark pass).

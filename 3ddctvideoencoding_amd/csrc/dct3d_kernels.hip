@@ -526,7 +526,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         last = m0 + 64 < n_marks ? E.mark[m0 + 64] : E.status[1];
     };
     // window of a group: first word w0 (the first mark's), the lane's mark relative to bit 32 w0, the
-    // words up to the end mark (+4 slack); its first NWP * 64 words requested (clamped into the stream)
+    // words up to the end mark (+5 slack: parse_win); its first NWP * 64 words requested (clamped into the stream)
     auto open_window = [&](int lane, uint64_t my, uint64_t last, uint64_t& w0, uint32_t& rel, uint64_t& span,
                            uint32_t (&t)[NWP]) {
         w0 = uniform_u64(my >> 5);  // lane 0's mark: lane 0 of a live group is always a real mark
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         // unused cubes of a partial last group) parses from the window's first bit, inside the window
         rel = my > w0 * 32 ? (uint32_t)(my - w0 * 32) : 0u;
         const uint64_t lw = uniform_u64(last);
-        span = (lw >> 5) + 4 - w0;
+        span = (lw >> 5) + 5 - w0;
 #pragma unroll
         for (int b = 0; b < NWP; b++) t[b] = E.words[min(w0 + (uint64_t)(b * 64 + lane), E.n_words - 1)];
     };
