@@ -66,6 +66,43 @@ def alternatives(depth: int, n_random: int = 24, seed: int = 4):
     return alts
 
 
+def fdlibm_cos_ulp() -> dict:
+    """{argument: +-1} of the fdlibm plan: the arguments of the 8- and 4-point axes where fdlibm's cos
+    (tools/fdlibm_cos.py: StrictMath.cos, HotSpot's SharedRuntime::dcos) differs from glibc's, each by
+    exactly one ulp -- the plan of a JVM whose Math.cos is fdlibm's."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import fdlibm_cos
+    out = {}
+    for a in sorted(set(cos_args(8)) | set(cos_args(4))):
+        f, g = fdlibm_cos.cos(a), math.cos(a)
+        if f != g:
+            d = 1 if f > g else -1
+            assert f == math.nextafter(g, math.inf if d > 0 else -math.inf), a  # one ulp apart
+            out[a] = d
+    return out
+
+
+def fdlibm_study(quick: bool = False, log=print):
+    """changed quantised outputs / decoded bytes of every corpus under the fdlibm plan (both depths)"""
+    cu = fdlibm_cos_ulp()
+    res = {"fdlibm_vs_glibc_arguments": {repr(a): d for a, d in cu.items()}}
+    for depth in (8, 4):
+        base = oracle.Plan(8, 8, depth)
+        alt = oracle.Plan(8, 8, depth, cos_ulp=cu)
+        per = {}
+        for name, fr in corpora(depth, quick):
+            c = Corpus(name, fr, base)
+            ne, nd, dv = c.run(alt)
+            per[name] = {"coefficients": c.n_enc, "pixels": c.n_dec, "changed_encode": ne, "changed_decode": nd}
+            log(f"  [{depth}] {name}: fdlibm plan changes {ne} of {c.n_enc} quantised outputs, {nd} of {c.n_dec} bytes")
+        tot = sum(v["coefficients"] for v in per.values())
+        ch = sum(v["changed_encode"] for v in per.values())
+        res[f"depth{depth}"] = {"corpora": per, "total_coefficients": tot, "changed_encode": ch,
+                                "changed_decode": sum(v["changed_decode"] for v in per.values()),
+                                "encode_per_1e8": ch / tot * 1e8}
+    return res
+
+
 def corpora(depth: int, quick: bool = False):
     """(name, frames u8 [F, H, W]) -- the committed golden fixtures' inputs and the digest stacks."""
     out = [("64x64 ramp", syn.frames(64, 64, depth, kind="ramp")),
@@ -198,7 +235,17 @@ def main():
     ap.add_argument("--quick", action="store_true", help="64x64 corpora only")
     ap.add_argument("--random", type=int, default=24)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fdlibm", action="store_true", help="only the fdlibm plan (StrictMath.cos)")
     a = ap.parse_args()
+    if a.fdlibm:
+        r = fdlibm_study(a.quick)
+        print(json.dumps({k: (v if k.startswith("fd") else {kk: vv for kk, vv in v.items() if kk != "corpora"})
+                          for k, v in r.items()}))
+        if a.out:
+            os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+            with open(a.out, "w") as f:
+                json.dump(r, f, indent=1)
+        return
     out = {}
     for depth in (8, 4):
         t0 = time.time()
