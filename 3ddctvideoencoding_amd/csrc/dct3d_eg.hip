@@ -347,8 +347,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 constexpr uint64_t kChunkBits = kEgChunkBits;
 constexpr uint64_t kNoExit = ~0ull;
 // a block's window: its 256 chunks plus slack (a parse ends < 27 bits past its chunk; the reader's
-// buffer and the long-code path look < 96 bits ahead of its position)
+// buffer and the long-code path look < 96 bits ahead of its position), in groups of 32 chunks stored
+// transposed (win_at, dct3d_eg_bits.h)
 constexpr uint32_t kSyncWinWords = kEgBlock * (uint32_t)(kChunkBits / 32) + 8;
+// win_at of the last slack word, + 1, + the mark pass's dummies (eg_mark_kernel: 16 dwords of each slack row)
+constexpr uint32_t kSyncWinAlloc = kSlackRows + 7 * 32 + 17;
+static_assert(kChunkBits == 512 && kEgBlock == 256, "16-word chunks, 8 groups of 32 and the slack chunk");
 constexpr uint32_t kMarkVals = 32;          // values per emit lane / per mark
 constexpr uint32_t kEmitWinWords = 2048;    // per wave: window (<= 2,048 values x 27 bits) / 8 KiB staging
 
@@ -359,31 +363,46 @@ __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t
     return e == kNoExit ? P.start_bit + t * kChunkBits : e;
 }
 
-// the block's window: chunks [first, first + kEgBlock) plus slack, coalesced, then a barrier
-// (NT threads: the single-chain passes run 256, the two-chain ones 128)
-template <uint32_t NT = kEgBlock>
+// The block's window (chunks [first, first + kEgBlock) and 8 slack words), then a barrier.  Thread t
+// loads its own chunk's 16 words as four 16-byte loads (all in flight at once) and writes word j of it to
+// its column (col_base(t) + 32 j): the 32 stores of a half-wave fall on 32 consecutive dwords, no bank
+// conflict.  (Rounds 1-4: 17 coalesced dword loads per thread, thread i storing word i + 256 b of the
+// linear window; the four 16-byte loads made the sync pass 422 -> 405 us, the mark pass -15 us.)
+// Threads 0 and 1 also take the slack chunk's two quarters.  The data's last window (zeros past the
+// end) takes single predicated loads.
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win, uint64_t first) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
     const uint64_t w0 = (P.start_bit + first * kChunkBits) >> 5;
-    // all of a thread's loads in flight at once (clamped, unconditional): the one-word loop under a
-    // bounds branch waited out a full global round trip per 256 words, 17 per block
-    constexpr uint32_t kR = (kSyncWinWords + NT - 1) / NT;
-    if (P.n_words) {  // block-uniform
-        uint32_t t[kR];
+    const uint32_t t = threadIdx.x;
+    const bool slack = t < 2;  // quarter t of the slack chunk (kEgBlock)
+    u32x4 v[5];
+    if (w0 + kSyncWinWords <= P.n_words) {  // block-uniform
+        const uint32_t* src = P.words + w0;
 #pragma unroll
-        for (uint32_t b = 0; b < kR; b++) t[b] = P.words[min(w0 + threadIdx.x + b * NT, P.n_words - 1)];
-#pragma unroll
-        for (uint32_t b = 0; b < kR; b++) {
-            const uint32_t i = threadIdx.x + b * NT;
-            if (i < kSyncWinWords) win[i] = w0 + i < P.n_words ? __builtin_bswap32(t[b]) : 0u;
-        }
+        for (uint32_t q = 0; q < 4; q++) v[q] = *(const u32x4*)(src + 16 * t + 4 * q);
+        v[4] = slack ? *(const u32x4*)(src + 16 * kEgBlock + 4 * t) : u32x4{0u, 0u, 0u, 0u};
     } else {
-        for (uint32_t i = threadIdx.x; i < kSyncWinWords; i += NT) win[i] = 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 5; q++) {
+            const uint64_t k0 = w0 + (q < 4 ? 16 * t + 4 * q : 16 * kEgBlock + 4 * t);
+#pragma unroll
+            for (uint32_t e = 0; e < 4; e++)
+                v[q][e] = k0 + e < P.n_words && (q < 4 || slack) ? P.words[k0 + e] : 0u;
+        }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++)
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) win[col_base(t) + (4 * q + e) * kColStride] = __builtin_bswap32(v[q][e]);
+    if (slack) {
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) win[win_at(16 * kEgBlock + 4 * t + e)] = __builtin_bswap32(v[4][e]);
     }
     __syncthreads();
     return LdsBits{win, w0, kSyncWinWords};
 }
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win) {
-    return stage_block_window<kEgBlock>(P, win, (uint64_t)blockIdx.x * kEgBlock);
+    return stage_block_window(P, win, (uint64_t)blockIdx.x * kEgBlock);
 }
 
 // window-relative form of an absolute bit position (clamped: positions past the window behave as the
@@ -431,7 +450,29 @@ __device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
     r.avail = (int)c.avail;
     r.next = c.nx;
     r.pos = c.pos();
-    r.pre = r.s[c.nx < r.n ? c.nx : 0u];
+    r.pre = r.s[win_at(c.nx < r.n ? c.nx : 0u)];
+}
+
+// Window word readers of the lean steps.  ColRead: the thread's own chunk, word j (< 16) of it at
+// col[32 j] (win_at: chunk c's column starts at (c >> 5) * 512 + (c & 31)) -- one v_lshl_add per read, as
+// the linear window's address, and a half-wave's reads fall on 32 distinct banks whatever their offsets.
+// The interior loops use it in chunk-relative coordinates (bit 0 = the chunk's first bit): they stop
+// kLeanMargin bits before the chunk end, so a step never reads past word 14 (kLeanMargin below).
+// WinRead: any window word i (win_at, 5 VALU: the bounded steps at the chunk end).
+struct ColRead {
+    const uint32_t* col;
+    __device__ __forceinline__ uint32_t operator()(uint32_t j) const { return col[j * kColStride]; }
+};
+struct WinRead {
+    const uint32_t* s;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return s[win_at(i)]; }
+};
+__device__ __forceinline__ ColRead col_of(const uint32_t* win, uint32_t lc) { return ColRead{win + col_base(lc)}; }
+// Lean state moved between window coordinates and the chunk's own (bit 0 = the chunk's first bit, word 0 =
+// its first word): only nx changes
+__device__ __forceinline__ Lean lean_rebase(Lean c, int32_t dwords) {
+    c.nx += (uint32_t)dwords;
+    return c;
 }
 
 // One branchless step inside the interior (every word read lies in the window): a run of 1-bit codes
@@ -443,8 +484,8 @@ __device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
 // so the parse ends exactly at the first code boundary at or past the stop (the code may reach past).
 // CAP: the run's cap when unbounded (31; the mark pass's two-code step: 30, so that a step takes <= 32
 // values).  n1_out / w_out: the run's length and the code's width (0: none).
-template <bool BOUNDED = false, uint32_t CAP = 31u>
-__device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& bad, uint32_t room = 32u,
+template <bool BOUNDED = false, uint32_t CAP = 31u, class Rd>
+__device__ __forceinline__ uint32_t lean_step(const Rd& s, Lean& c, bool& bad, uint32_t room = 32u,
                                               uint32_t* n1_out = nullptr, uint32_t* w_out = nullptr) {
     // ones at the top of hi, at most CAP (BOUNDED: at most room): the OR-ed bit makes clz defined and caps it
     const uint32_t cap_bit = BOUNDED ? 0x80000000u >> min(room, 31u) : 0x80000000u >> CAP;
@@ -463,7 +504,7 @@ __device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& 
     lo = need ? rl : lo;
     c.avail += need ? 32u : 0u;
     c.nx += need ? 1u : 0u;
-    c.pre = s[c.nx];
+    c.pre = s(c.nx);
     const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
     bad = has && zz >= 16u;
     const bool take = has && zz < 16u;
@@ -479,10 +520,15 @@ __device__ __forceinline__ uint32_t lean_step(const uint32_t* s, Lean& c, bool& 
 // lean_step, then a second code when it lies wholly in the buffered bits (no refill between): dense
 // content (few 1-bit codes, the steps mostly a run of 0-1 and one code) takes two codes per step.  A step
 // moves at most CAP + 31 + 31 bits and CAP + 2 values; the second code starts at bit n1 + w of the step.
-template <uint32_t CAP = 31u>
-__device__ __forceinline__ uint32_t lean_step2(const uint32_t* s, Lean& c, bool& bad, uint32_t* n1_out = nullptr,
+// The interior loops run while the parse is kLeanMargin bits short of every bound: a step then moves at
+// most 93 bits and reads the word that starts at most 31 + 63 bits past its position (the refill leaves
+// avail < 64), so neither its bits nor its read reach the bound (nor, in chunk coordinates, word 15).
+constexpr uint32_t kLeanMargin = 128;
+static_assert(31 + 31 + 31 < kLeanMargin && 31 + 63 + 32 <= kLeanMargin, "lean steps stay inside the margin");
+template <uint32_t CAP = 31u, class Rd>
+__device__ __forceinline__ uint32_t lean_step2(const Rd& s, Lean& c, bool& bad, uint32_t* n1_out = nullptr,
                                                uint32_t* w_out = nullptr) {
-    const uint32_t n = lean_step<false, CAP>(s, c, bad, 32u, n1_out, w_out);
+    const uint32_t n = lean_step<false, CAP, Rd>(s, c, bad, 32u, n1_out, w_out);
     // bits past avail are zero: a code whose leading zeros run past them is not taken (w2 > avail)
     const uint32_t z2 = (uint32_t)__builtin_clz(c.hi | 1u);
     const uint32_t w2 = 2u * z2 + 1u;
@@ -551,7 +597,7 @@ __device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, u
 // chunk, in place; only if that exit differs from the pass-0 exit (which chunk t + 1 resolved against)
 // is status[0] set, and the host then runs confirming passes (iteration 1, plain mapping).
 __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
-    __shared__ uint32_t win[kSyncWinWords];
+    __shared__ uint32_t win[kSyncWinAlloc];
     __shared__ uint32_t s_exit[kEgBlock];
     const bool rs = iteration == 0 && resolve;
     const uint64_t b = blockIdx.x;
@@ -571,16 +617,21 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     if (live) {
         r.seek(s0);
         // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary.
-        // The chunk interior first, without bounds (a step moves at most 31 + 31 bits), then the checked
-        // steps; a long or invalid code leaves the lean loop unconsumed.
-        const uint32_t fast_stop = stop > 128u ? stop - 128u : 0u;
+        // The chunk interior first, without bounds (kLeanMargin), then the bounded steps to the chunk end,
+        // then the checked steps; a long or invalid code leaves the lean loops unconsumed.
+        // (the interior in the chunk's own coordinates, reading its column; lc: the chunk's index in the
+        // window -- threadIdx.x, but for block 0's resolving pass threadIdx.x - 1)
+        const uint32_t lc = (uint32_t)(t - first), cb = kChunkBits * lc;
+        const uint32_t fast_stop = stop > cb + kLeanMargin ? stop - cb - kLeanMargin : 0u;
         // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
         // chunk end (a code running past the limit is invalid: the checked steps)
         const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
-        Lean c = lean_from(r);
+        Lean c = lean_rebase(lean_from(r), -(int32_t)(16 * lc));
         bool bad = false;
-        while (!bad & (c.pos() < fast_stop)) n += lean_step2(win, c, bad);
-        while (!bad & (c.pos() < bstop)) n += lean_step<true>(win, c, bad, bstop - c.pos());
+        const ColRead col = col_of(win, lc);
+        while (!bad & (c.pos() < fast_stop)) n += lean_step2(col, c, bad);
+        c = lean_rebase(c, 16 * lc);
+        while (!bad & (c.pos() < bstop)) n += lean_step<true>(WinRead{win}, c, bad, bstop - c.pos());
         lean_to(r, c);
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
         }
@@ -609,10 +660,16 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
 // to back, so that the L2 assembles whole lines: WRITE_SIZE 1.67 GB -> 0.52 GB (the marks' own bytes) and
 // the pass 708 -> 529 us on one box (round 4; stored one at a time as the parse reached them, through a
 // buffer descriptor, each lane's marks tens of microseconds apart, the lines were written back partial).
-// The slots cost 9 KiB per block (6 blocks per CU instead of 8).
-constexpr uint32_t kMkSlot = 18;  // a chunk has at most 17 marks (<= 512 values); entry 17: the dummy
+// The slots cost 8.5 KiB per block (with the window, 6 blocks per CU instead of 8).  A step's one possible
+// mark is stored branch-free: steps without a mark store to the thread's dummy dword in an unused slot of
+// the window (row t / 16, column kEgBlock + 1 + t % 16; round 4: an 18th slot entry, which with the
+// transposed window's 2 KiB would have cost a block per CU; an exec-masked store instead of the dummy
+// compiled to a branch and 13 more VALU per step).
+// Marks leave as the low 32 bits of their bit position (round 5; 64-bit before: 0.52 GB written and read
+// back per c8 step), the whole position of every 64th (a consumer group's first) in mark_base.
+constexpr uint32_t kMkSlot = 17;  // a chunk has at most 17 marks (<= 512 values)
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
-    __shared__ uint32_t win[kSyncWinWords];
+    __shared__ uint32_t win[kSyncWinAlloc];
     __shared__ uint16_t s_mk[kEgBlock * kMkSlot];
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
     // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
@@ -638,6 +695,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t sp = rel_bit(s, base);  // the chunk's true start (LDSM marks are relative to it)
     r.seek(sp);
     uint16_t* const myk = s_mk + threadIdx.x * kMkSlot;  // mark k of the chunk (value 32 k - ph) at myk[k]
+    // a step without a mark stores to the thread's dummy: half of a dword in an unused column (1 .. 16) of
+    // the slack rows (row threadIdx.x / 32)
+    uint16_t* const dummy = (uint16_t*)(win + kSlackRows + 32 * (threadIdx.x >> 5) + 1 + ((threadIdx.x & 31) >> 1)) +
+                            (threadIdx.x & 1);
     // chunk-relative 32-bit value count i (value idx0 + i): the 64-bit index arithmetic per step was a
     // large part of the pass.  A chunk holds at most ~kChunkBits + 64 codes, so rem below never binds
     // unless the wanted values end inside this chunk.
@@ -645,22 +706,25 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t rem = (uint32_t)min(rem64, (uint64_t)(2 * kChunkBits));
     const bool ends_here = rem64 <= 2 * kChunkBits;
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
-    uint64_t* const mk = P.mark + (idx0 / kMarkVals);  // mark[(idx0 + i) / 32] = mk[(ph + i) / 32]
+    const uint64_t gm0 = idx0 / kMarkVals;  // mark gm0 + k = mark of value idx0 + 32 k - ph
     uint32_t i = 0, code;
-    // Interior of the chunk: a step moves at most 31 + 31 bits and 32 values, so while the parse is
-    // 128 bits short of the chunk end and of the data limit, and 66 values short of the wanted count,
+    // Interior of the chunk: a step moves at most 30 + 31 + 31 bits and 32 values, so while the parse is
+    // kLeanMargin bits short of the chunk end and of the data limit, and 66 values short of the wanted count,
     // none of the bounds below can bind -- a lean loop without them (a long or invalid code leaves it for
     // the checked loop, which reads or reports it).
     const uint32_t lim_end = min(end, limit);
-    const uint32_t fast_end = lim_end > 128u ? lim_end - 128u : 0u;
+    const uint32_t cb = kChunkBits * threadIdx.x;  // the chunk's first bit (the interior's coordinates)
+    const uint32_t fast_end = lim_end > cb + kLeanMargin ? lim_end - cb - kLeanMargin : 0u;
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
     {
-        Lean c = lean_from(r);
+        Lean c = lean_rebase(lean_from(r), -(int32_t)(16 * threadIdx.x));
         bool bad = false;
+        const ColRead col = col_of(win, threadIdx.x);
+        const uint32_t spc = sp - cb;
         // a step takes nv <= 32 values, value i + d at bit p0 + d: at most one mark, value i + d0
         auto mark = [&](uint32_t p0, uint32_t nv) {
             const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
-            myk[d0 < nv ? (ph + i + d0) / kMarkVals : kMkSlot - 1] = (uint16_t)(p0 + d0 - sp);  // no branch
+            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(p0 + d0 - sp);  // no branch
             i += nv;
         };
         // two-code steps (a run of <= 30, a code, a second code when buffered: nv <= 32): value i + d at bit
@@ -668,18 +732,19 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
         while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
             const uint32_t p0 = c.pos();
             uint32_t n1, w;
-            const uint32_t nv = lean_step2<30u>(win, c, bad, &n1, &w);
+            const uint32_t nv = lean_step2<30u>(col, c, bad, &n1, &w);
             const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
             const uint32_t at = p0 + d0 + (d0 > n1 ? w - 1u : 0u);
-            myk[d0 < nv ? (ph + i + d0) / kMarkVals : kMkSlot - 1] = (uint16_t)(at - sp);  // no branch
+            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(at - spc);  // no branch
             i += nv;
         }
+        c = lean_rebase(c, 16 * threadIdx.x);
         // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
         // end take the checked steps)
         const uint32_t bend = limit >= end + 64u ? end : 0u;
         while (!bad & (c.pos() < bend) & (i < fast_rem)) {
             const uint32_t p0 = c.pos();
-            mark(p0, lean_step<true>(win, c, bad, bend - p0));
+            mark(p0, lean_step<true>(WinRead{win}, c, bad, bend - p0));
         }
         lean_to(r, c);
     }
@@ -713,7 +778,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     }
     // the chunk's marks k = (ph ? 1 : 0) .. (ph + i - 1) / 32, back to back
     const uint64_t b0 = base + sp;
-    for (uint32_t k = ph ? 1u : 0u; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) mk[k] = b0 + myk[k];
+    uint32_t* const mk = P.mark + gm0;
+    for (uint32_t k = ph ? 1u : 0u; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) {
+        const uint64_t m = b0 + myk[k];
+        mk[k] = (uint32_t)m;
+        if (((gm0 + k) & (kMarkGroup - 1)) == 0) P.mark_base[(gm0 + k) / kMarkGroup] = m;
+    }
 }
 
 template <int D>
@@ -730,9 +800,11 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const uint64_t m0 = ((uint64_t)blockIdx.x * kEgWaves + wave) * 64;
     if (m0 >= n_marks) return;
     const bool lv = m0 + lane < n_marks;
-    const uint64_t my = lv ? P.mark[m0 + lane] : 0;
-    const uint64_t first = __shfl(my, 0, 64);
-    const uint64_t last = m0 + 64 < n_marks ? P.mark[m0 + 64] : P.status[1];  // wave-uniform
+    static_assert(kMarkGroup == 64, "a wave = one mark group");
+    const uint64_t gb = P.mark_base[m0 / kMarkGroup];  // wave-uniform
+    const uint64_t my = lv ? mark_at(P, m0 + lane, gb) : 0;
+    const uint64_t first = gb;
+    const uint64_t last = m0 + 64 < n_marks ? P.mark_base[m0 / kMarkGroup + 1] : P.status[1];  // wave-uniform
     const uint64_t w0 = first >> 5;
     const uint64_t span = (last >> 5) + 5 - w0;  // + 5 words of slack: parse_win
     const bool fits = span <= kEmitWinWords - 1;  // wave-uniform

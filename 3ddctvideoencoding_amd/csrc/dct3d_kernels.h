@@ -91,6 +91,10 @@ struct EgParams {
 
 // Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)
 constexpr uint64_t kEgChunkBits = 512;  // bits per parse chunk (one thread each)
+// Marks (the bit position of every 32nd value) are stored as 32-bit low halves; the marks of a group of
+// kMarkGroup (a consumer wave's 2,048 values) lie within 2^32 bits of the group's first (a value's code
+// has < 64 bits), whose whole position is kept in mark_base: mark_at() rebuilds a 64-bit position.
+constexpr uint64_t kMarkGroup = 64;
 struct EgDecParams {
     const uint32_t* words;     // stream, memory byte order
     uint64_t n_words;
@@ -104,7 +108,8 @@ struct EgDecParams {
     uint32_t* count;           // codewords per chunk
     uint64_t* off;             // value index of each chunk's first codeword (scan)
     uint64_t* status;          // [0] changed / first invalid chunk, [1] end bit, [2] flags 1 corrupt, [3] values
-    uint64_t* mark;            // [n_values / 32] bit position of every 32nd value
+    uint32_t* mark;            // [n_values / 32] bit position of every 32nd value, low 32 bits
+    uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output
 };
 
@@ -123,6 +128,11 @@ struct EgFusedParams {
     uint32_t seg_cap;          // 64 * words per lane (worst case cs/8 values x 27 bits)
     uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
 };
+
+// the whole bit position of mark m (its group's base: mark_base[m / kMarkGroup], read once per group)
+__device__ __forceinline__ uint64_t mark_at(const EgDecParams& P, uint64_t m, uint64_t group_base) {
+    return group_base + (uint32_t)(P.mark[m] - (uint32_t)group_base);
+}
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
 int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st);

@@ -453,13 +453,15 @@ template <int D>
 struct ReloadStream {
     const uint32_t* words;
     uint64_t n_words;
-    const uint64_t* mark;
+    const uint32_t* mark;
+    const uint64_t* mark_base;
     const uint16_t* diag;  // the block's LDS copy
     __device__ __forceinline__ void operator()(uint32_t g, double* cf, int lane) const {
         constexpr int PARTS = 64 * D / 32;
         if (lane < PARTS) {
             BitReader<GlobalBits> r{GlobalBits{words, n_words}, 0, 0, 0, 0};
-            r.seek(mark[(uint64_t)g * PARTS + lane]);
+            const uint64_t m = (uint64_t)g * PARTS + lane, gb = mark_base[m / kMarkGroup];
+            r.seek(gb + (uint32_t)(mark[m] - (uint32_t)gb));  // mark_at
             for (int i = 0; i < 32; i++) {
                 uint32_t code = 1u;
                 (void)r.get(code);
@@ -519,20 +521,27 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     const uint64_t n_marks = E.n_values / 32;
     const uint32_t row0 = xcd_tile() * NG;  // the block's first round of 4 groups
     auto cube_of = [&](int i) { return P.cube_base + ((row0 + (uint32_t)i) * kWavesPerBlock + wave) * CPW; };
-    // the group's marks: the lane's (value 32 * (m0 + lane)) and the end of its bit range (all lanes alike)
-    auto load_marks = [&](int lane, uint32_t cube0, uint64_t& my, uint64_t& last) {
+    // the group's marks as loaded: its first (a whole position), the lane's low 32 bits (value 32 * (m0 +
+    // lane); a lane past the last mark: the first's) and the end of its bit range (all lanes alike).  They
+    // are combined in open_window, after the parse they are loaded across (combined here, the wait for them
+    // sat before the parse)
+    static_assert(kMarkGroup == 64, "a group = one mark group");
+    auto load_marks = [&](int lane, uint32_t cube0, uint64_t& gb, uint32_t& myl, uint64_t& last) {
         const uint64_t m0 = (uint64_t)cube0 * CS / 32;
-        my = m0 + lane < n_marks ? E.mark[m0 + lane] : 0;
-        last = m0 + 64 < n_marks ? E.mark[m0 + 64] : E.status[1];
+        gb = E.mark_base[m0 / kMarkGroup];
+        myl = m0 + lane < n_marks ? E.mark[m0 + lane] : 0u;
+        last = m0 + 64 < n_marks ? E.mark_base[m0 / kMarkGroup + 1] : E.status[1];
     };
     // window of a group: first word w0 (the first mark's), the lane's mark relative to bit 32 w0, the
     // words up to the end mark (+5 slack: parse_win); its first NWP * 64 words requested (clamped into the stream)
-    auto open_window = [&](int lane, uint64_t my, uint64_t last, uint64_t& w0, uint32_t& rel, uint64_t& span,
-                           uint32_t (&t)[NWP]) {
-        w0 = uniform_u64(my >> 5);  // lane 0's mark: lane 0 of a live group is always a real mark
-        // < 2^17 for a real mark (a group spans < 2^17 bits); a lane past the last mark (my = 0: the
-        // unused cubes of a partial last group) parses from the window's first bit, inside the window
-        rel = my > w0 * 32 ? (uint32_t)(my - w0 * 32) : 0u;
+    auto open_window = [&](int lane, uint64_t gb, uint32_t myl, uint64_t last, uint64_t& w0, uint32_t& rel,
+                           uint64_t& span, uint32_t (&t)[NWP]) {
+        w0 = uniform_u64(gb >> 5);  // the group's first mark
+        // mark_at, relative to bit 32 w0: < 2^17 for a real mark (a group spans < 2^17 bits); a lane past
+        // the last mark (myl = 0, the unused cubes of a partial last group: ~2^32) parses from the window's
+        // first bit, inside the window
+        const uint64_t d = gb + (uint32_t)(myl - (uint32_t)gb) - w0 * 32;
+        rel = d < (1ull << 20) ? (uint32_t)d : 0u;
         const uint64_t lw = uniform_u64(last);
         span = (lw >> 5) + 5 - w0;
 #pragma unroll
@@ -542,10 +551,11 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     uint32_t rel;
     uint32_t pw[NWP];
     {
-        uint64_t my, last;
+        uint64_t gb, last;
+        uint32_t myl;
         __builtin_amdgcn_s_setprio(3);  // marks and window loads ahead of the computing waves
-        load_marks(lane0, cube_of(0), my, last);
-        open_window(lane0, my, last, w0, rel, span, pw);
+        load_marks(lane0, cube_of(0), gb, myl, last);
+        open_window(lane0, gb, myl, last, w0, rel, span, pw);
         __builtin_amdgcn_s_setprio(0);
     }
     for (int i = 0; i < NG; i++) {
@@ -574,12 +584,13 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
                 if (j < nwin) win[j] = w0 + j < E.n_words ? __builtin_bswap32(t[b]) : 0u;
             }
         }
-        uint64_t my_n = 0, last_n = 0;
-        if (i + 1 < NG) load_marks(lane, cube_of(i + 1), my_n, last_n);  // in flight during the parse
+        uint64_t gb_n = 0, last_n = 0;
+        uint32_t myl_n = 0;
+        if (i + 1 < NG) load_marks(lane, cube_of(i + 1), gb_n, myl_n, last_n);  // in flight during the parse
         wave_lds_sync();
         int32_t v[32];
         parse_values<32>(E, win, nwin, w0, fits, w0 * 32 + rel, v);
-        if (i + 1 < NG) open_window(lane, my_n, last_n, w0, rel, span, pw);  // in flight during the transform
+        if (i + 1 < NG) open_window(lane, gb_n, myl_n, last_n, w0, rel, span, pw);  // in flight during the transform
         wave_lds_sync();
         {  // each value to its diagonal position in the staging: 8 offsets per 16-byte table read
             const uint32_t c = lane / PARTS, part = lane % PARTS;
@@ -595,7 +606,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
             }
         }
         wave_lds_sync();
-        decode_tile<D, 1, (NG > 1)>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, s_diag});
+        decode_tile<D, 1, (NG > 1)>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, E.mark_base, s_diag});
         // the region receives the next group's window: after a block store (its rows are read by every
         // wave of the block) the whole block must be past it (block-uniform condition, as dec_store_tile's)
         if (i + 1 < NG) {

@@ -275,8 +275,9 @@ int dct3d_ctx_set_stream(dct3d_ctx* c, void* s) {
         if (hipEventRecord(c->ev_switch, c->stream) == hipSuccess) {
             if (hipStreamWaitEvent(ns, c->ev_switch, 0) != hipSuccess) return DCT3D_EDEVICE;
         } else {
-            // the old stream is gone (a caller's short-lived stream destroyed before the switch): its
-            // work was still ordered by a device-wide synchronisation, which covers it either way
+            // HIP rejected the old handle (a caller's stream destroyed before the switch, against the
+            // contract in dct3d.h): order by a device-wide synchronisation.  A destroyed handle that HIP
+            // has reused for a new stream is not detectable here -- hence the contract.
             (void)hipGetLastError();
             if (hipDeviceSynchronize() != hipSuccess) return DCT3D_EDEVICE;
         }
@@ -959,7 +960,9 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     if (!rc) rc = c->d_eg_bits.grow(n_chunks * sizeof(uint32_t));
     if (!rc) rc = c->d_eg_off.grow(n_chunks * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
-    if (!rc) rc = c->d_egd_mark.grow((n_cubes * (uint64_t)c->plan.cs / 32 + 1) * sizeof(uint64_t));
+    const uint64_t n_marks = n_cubes * (uint64_t)c->plan.cs / 32;
+    const uint64_t n_mark_groups = n_marks / kMarkGroup + 1;
+    if (!rc) rc = c->d_egd_mark.grow(n_mark_groups * sizeof(uint64_t) + (n_marks + 1) * sizeof(uint32_t));
     if (rc) return rc;
     D.words = (const uint32_t*)d_bytes;
     D.n_words = (nbytes + 3) / 4;
@@ -973,7 +976,8 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.count = (uint32_t*)c->d_eg_bits.p;
     D.off = (uint64_t*)c->d_eg_off.p;
     D.status = (uint64_t*)c->d_egd_status.p;
-    D.mark = (uint64_t*)c->d_egd_mark.p;
+    D.mark_base = (uint64_t*)c->d_egd_mark.p;
+    D.mark = (uint32_t*)(D.mark_base + n_mark_groups);
     D.q = nullptr;
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts and, resolving,
     // usually proves every chunk in sync by itself; otherwise confirming passes follow); at most

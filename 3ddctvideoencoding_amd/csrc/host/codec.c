@@ -15,9 +15,9 @@
  * batches go round-robin to the devices, each coded from a zero carry; the calling thread joins the
  * batch streams in order, shifting each by the running partial byte, into the one zlib stream -- the
  * same .bin as encode_ex.  Decode: a batch's first bit is known only when the previous batch is
- * decoded (the stream has no index), so the device calls chain; the devices alternate so that one
- * batch's decode runs while the calling thread inflates the next window and writes the previous
- * raster. */
+ * decoded (the stream has no index), so the device calls chain and alternate over the devices; the only
+ * overlap is the previous batch's raster write (several devices) -- the next window is inflated after
+ * the running decode returns.  Decoding does not get faster with more devices. */
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>

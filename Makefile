@@ -11,7 +11,7 @@ LIBDIR  := $(PKG)/lib
 OBJ     := build/obj
 # -ffp-contract=off: the certification bounds (dct3d_plan.cpp) are derived for exactly the written
 # operation sequence; no FMA contraction behind its back.
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function -Iinclude
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -ffp-contract=off -fPIC -Wall -Wno-unused-function -Iinclude $(EXTRA_HIPFLAGS)
 CFLAGS   := -O2 -fPIC -Wall -Wextra -Wno-unused-parameter -Iinclude -std=c11 -D_GNU_SOURCE
 
 DEV_SRCS  := $(CSRC)/dct3d_kernels.hip $(CSRC)/dct3d_kernels_f.hip $(CSRC)/dct3d_eg.hip

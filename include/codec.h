@@ -38,8 +38,9 @@ int decode_ex(const char *inputFileName, const char *outputFileName, int width, 
 /* Several devices (platformIndices[0 .. nDevices-1], 1-based; a device may repeat), one host thread and
  * one context each.  encode_multi: batches round-robin over the devices, their streams joined in order:
  * the same .bin as encode_ex.  decode_multi: the batches' device decodes chain on the stream position
- * (the stream has no index) and alternate over the devices, overlapping the inflate of the next window
- * and the write of the previous raster.  Same return convention. */
+ * (the stream has no index) and alternate over the devices; only the previous batch's raster write
+ * overlaps a decode (with two or more devices), so decoding does not scale with devices.  Same return
+ * convention. */
 int encode_multi(const char *inputFileName, const char *outputFileName, int width, int height, int framesToEncode,
                  const int *platformIndices, int nDevices, int blockDepth, int stacksPerBatch);
 int decode_multi(const char *inputFileName, const char *outputFileName, int width, int height, int framesToDecode,

@@ -115,8 +115,10 @@ void dct3d_ctx_destroy(dct3d_ctx *ctx);
 
 /* Use an external hipStream_t (e.g. a framework's current stream) instead of the ctx-owned one.
  * NULL restores the ctx-owned stream.  Work enqueued afterwards is ordered after the previous
- * stream's work (an event on it; should that stream already be destroyed, a device-wide
- * synchronisation instead). */
+ * stream's work by an event recorded on the previous stream, which therefore MUST STILL EXIST when
+ * this is called: switch away from a caller's stream before destroying it.  (Should HIP reject the
+ * previous handle, a device-wide synchronisation orders the work instead -- but a destroyed stream's
+ * handle may already name a new stream, so that is no guarantee.) */
 int dct3d_ctx_set_stream(dct3d_ctx *ctx, void *hip_stream);
 /* The ctx's device ordinal, block depth and the hipStream_t its calls run on (any pointer may be
  * NULL).  Lets companion libraries (libdct3d_diag.so) queue work in order with the ctx's. */

@@ -350,3 +350,20 @@ def test_parallel_deflate_single_thread_is_reference_bytes(pkg, plan8):
     fr = pkg.synthetic.frames(64, 48, 16, kind="ramp")
     q = plan8.encode_q(fr).reshape(-1)
     assert entropy_encode_mt(pkg, q, 64, 48, 2, 8, 1, 0) == entropy_encode(pkg, q, 64, 48, 2, 8)
+
+
+@pytest.mark.parametrize("devices,ok", [("1", True), ("1,2,3", True), ("1,,2", False), ("1,x", False),
+                                         ("0", False), ("-1", False), ("", False), ("2,", False),
+                                         (",".join(["1"] * 65), False)])
+def test_cli_device_list_parsing(devices, ok, tmp_path):
+    """the CLI's device list (main.c) rejects empty, non-numeric, non-positive entries and lists
+    longer than 64 with the usage text, instead of mapping them to device 1 / truncating (no GPU needed:
+    a valid list fails later, at the missing input file)."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3ddctvideoencoding_amd", "lib",
+                       "dct3d_codec")
+    r = subprocess.run([cli, "encode", str(tmp_path / "missing.raw"), str(tmp_path / "o.bin"), "64", "64", "8", devices],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1
+    assert ("Invalid device list" in r.stdout) == (not ok), r.stdout
+    assert ("Usage" in r.stdout) == (not ok)
