@@ -248,6 +248,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
     const uint64_t g = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (g >= P.n_cubes) return;
     const uint64_t start = P.off[g], end = start + P.bits[g];
+    if (end == start) return;  // never for a coded cube or segment (>= 256 bits); no word to place
     const uint64_t w0 = start >> 5, wl = (end - 1) >> 5;
     uint32_t first = P.head[g];
     if (g == 0) first |= P.carry_byte & (0xFF00u >> P.carry_bits);  // stream byte 0 = memory byte 0
@@ -267,8 +268,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
 // eg_write_kernel.  (Round 4 before: lane-local words in slot columns and a lane bit-count array, the
 // lanes concatenated here through shuffles and an LDS image: 275 us per c7 step, 0.42 GB of slot reads;
 // one segment per wave: 201 us, two dependent round trips per 180 words.)
-constexpr int kCompactPF = 4;   // rows of 64 words per segment per load round trip
-constexpr int kCompactSPW = 4;  // segments per wave
+// kCompactSPW segments per wave, kCompactPF rows of 64 words per segment per load round trip: 4 x 4
+// for 8x8x4's 8-cube segments, 8 x 2 for 8x8x8's 4-cube ones
+template <int kCompactSPW, int kCompactPF>
 __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
                                                               uint32_t seg_cap) {
     if (P.status[1] != 0) return;  // capacity failure: nothing is written
@@ -347,12 +349,11 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 constexpr uint64_t kChunkBits = kEgChunkBits;
 constexpr uint64_t kNoExit = ~0ull;
 // a block's window: its 256 chunks plus slack (a parse ends < 27 bits past its chunk; the reader's
-// buffer and the long-code path look < 96 bits ahead of its position), in groups of 32 chunks stored
-// transposed (win_at, dct3d_eg_bits.h)
+// buffer and the long-code path look < 96 bits ahead of its position); behind it the mark pass's dummies
+// (eg_mark_kernel: 2 bytes per thread)
 constexpr uint32_t kSyncWinWords = kEgBlock * (uint32_t)(kChunkBits / 32) + 8;
-// win_at of the last slack word, + 1, + the mark pass's dummies (eg_mark_kernel: 16 dwords of each slack row)
-constexpr uint32_t kSyncWinAlloc = kSlackRows + 7 * 32 + 17;
-static_assert(kChunkBits == 512 && kEgBlock == 256, "16-word chunks, 8 groups of 32 and the slack chunk");
+constexpr uint32_t kSyncWinAlloc = kSyncWinWords + kEgBlock / 2;
+static_assert(kChunkBits == 512 && kEgBlock == 256, "16-word chunks");
 constexpr uint32_t kMarkVals = 32;          // values per emit lane / per mark
 constexpr uint32_t kEmitWinWords = 2048;    // per wave: window (<= 2,048 values x 27 bits) / 8 KiB staging
 
@@ -365,9 +366,8 @@ __device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t
 
 // The block's window (chunks [first, first + kEgBlock) and 8 slack words), then a barrier.  Thread t
 // loads its own chunk's 16 words as four 16-byte loads (all in flight at once) and writes word j of it to
-// its column (col_base(t) + 32 j): the 32 stores of a half-wave fall on 32 consecutive dwords, no bank
-// conflict.  (Rounds 1-4: 17 coalesced dword loads per thread, thread i storing word i + 256 b of the
-// linear window; the four 16-byte loads made the sync pass 422 -> 405 us, the mark pass -15 us.)
+// LDS as four 16-byte stores.  (Rounds 1-4: 17 coalesced dword loads per thread, thread i storing word
+// i + 256 b: the four 16-byte loads made the sync pass 422 -> 405 us, the mark pass 489 -> 471 us.)
 // Threads 0 and 1 also take the slack chunk's two quarters.  The data's last window (zeros past the
 // end) takes single predicated loads.
 __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win, uint64_t first) {
@@ -392,12 +392,11 @@ __device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint
     }
 #pragma unroll
     for (uint32_t q = 0; q < 4; q++)
-#pragma unroll
-        for (uint32_t e = 0; e < 4; e++) win[col_base(t) + (4 * q + e) * kColStride] = __builtin_bswap32(v[q][e]);
-    if (slack) {
-#pragma unroll
-        for (uint32_t e = 0; e < 4; e++) win[win_at(16 * kEgBlock + 4 * t + e)] = __builtin_bswap32(v[4][e]);
-    }
+        *(uint4*)(win + 16 * t + 4 * q) = make_uint4(__builtin_bswap32(v[q][0]), __builtin_bswap32(v[q][1]),
+                                                     __builtin_bswap32(v[q][2]), __builtin_bswap32(v[q][3]));
+    if (slack)
+        *(uint4*)(win + 16 * kEgBlock + 4 * t) = make_uint4(__builtin_bswap32(v[4][0]), __builtin_bswap32(v[4][1]),
+                                                            __builtin_bswap32(v[4][2]), __builtin_bswap32(v[4][3]));
     __syncthreads();
     return LdsBits{win, w0, kSyncWinWords};
 }
@@ -450,30 +449,15 @@ __device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
     r.avail = (int)c.avail;
     r.next = c.nx;
     r.pos = c.pos();
-    r.pre = r.s[win_at(c.nx < r.n ? c.nx : 0u)];
+    r.pre = r.s[c.nx < r.n ? c.nx : 0u];
 }
 
-// Window word readers of the lean steps.  ColRead: the thread's own chunk, word j (< 16) of it at
-// col[32 j] (win_at: chunk c's column starts at (c >> 5) * 512 + (c & 31)) -- one v_lshl_add per read, as
-// the linear window's address, and a half-wave's reads fall on 32 distinct banks whatever their offsets.
-// The interior loops use it in chunk-relative coordinates (bit 0 = the chunk's first bit): they stop
-// kLeanMargin bits before the chunk end, so a step never reads past word 14 (kLeanMargin below).
-// WinRead: any window word i (win_at, 5 VALU: the bounded steps at the chunk end).
-struct ColRead {
-    const uint32_t* col;
-    __device__ __forceinline__ uint32_t operator()(uint32_t j) const { return col[j * kColStride]; }
-};
+// The window word reader of the lean steps (a functor: the interior loops were measured with other window
+// layouts)
 struct WinRead {
     const uint32_t* s;
-    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return s[win_at(i)]; }
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return s[i]; }
 };
-__device__ __forceinline__ ColRead col_of(const uint32_t* win, uint32_t lc) { return ColRead{win + col_base(lc)}; }
-// Lean state moved between window coordinates and the chunk's own (bit 0 = the chunk's first bit, word 0 =
-// its first word): only nx changes
-__device__ __forceinline__ Lean lean_rebase(Lean c, int32_t dwords) {
-    c.nx += (uint32_t)dwords;
-    return c;
-}
 
 // One branchless step inside the interior (every word read lies in the window): a run of 1-bit codes
 // (value 0) of up to 31 -- a run never extends past avail, whose bits are zero -- then a refill to >= 32
@@ -541,6 +525,60 @@ __device__ __forceinline__ uint32_t lean_step2(const Rd& s, Lean& c, bool& bad, 
     return n + (take2 ? 1u : 0u);
 }
 
+// Sync-pass step by table (round 5): a run of 1-bit codes as lean_step, a refill to >= 32 bits, then every
+// code that lies wholly in the next kEgLutBits bits at once, from a 4 KiB table of (codes, bits) per bit
+// pattern; no code complete in them (a code of more than kEgLutBits bits): one code by its leading zeros.
+// A step moves at most 31 + 31 bits (the lean loops' margin holds).  The sync pass needs only the count
+// and the exit, so the codes' individual boundaries are never formed.
+constexpr int kEgLutBits = 12;
+struct EgLut {
+    uint8_t e[1 << kEgLutBits];  // codes complete within the pattern (low 4 bits), the bits they take (high 4)
+};
+constexpr EgLut make_eg_lut() {
+    EgLut t{};
+    for (int v = 0; v < (1 << kEgLutBits); v++) {
+        int p = 0, k = 0;
+        for (;;) {
+            int z = 0;
+            while (p + z < kEgLutBits && !((v >> (kEgLutBits - 1 - p - z)) & 1)) z++;
+            if (p + 2 * z + 1 > kEgLutBits) break;
+            p += 2 * z + 1;
+            k++;
+        }
+        t.e[v] = (uint8_t)(k | (p << 4));
+    }
+    return t;
+}
+__device__ constexpr EgLut kEgLut = make_eg_lut();
+static_assert(kEgLutBits <= 15, "counts and widths fit 4 bits");
+
+template <class Rd>
+__device__ __forceinline__ uint32_t lean_step_lut(const Rd& s, const uint8_t* lut, Lean& c, bool& bad) {
+    const uint32_t n1 = __builtin_clz(~c.hi | 1u);  // run of 1-bit codes, at most 31, never past avail
+    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
+    c.avail -= n1;
+    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
+    const bool need = c.avail < 32u;  // refill (as lean_step): the run ended on a code boundary either way
+    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
+    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);
+    hi = need ? rh : hi;
+    lo = need ? rl : lo;
+    c.avail += need ? 32u : 0u;
+    c.nx += need ? 1u : 0u;
+    c.pre = s(c.nx);
+    const uint32_t e = lut[hi >> (32 - kEgLutBits)];
+    const uint32_t k = e & 15u;
+    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
+    const bool one = k == 0u && zz < 16u;  // one code of 13 .. 31 bits
+    bad = k == 0u && zz >= 16u;            // >= 33 bits or invalid: the checked loop reads it
+    const uint32_t w = k ? e >> 4 : (one ? 2u * zz + 1u : 0u);
+    b = (((uint64_t)hi << 32) | lo) << w;
+    c.hi = (uint32_t)(b >> 32);
+    c.lo = (uint32_t)b;
+    c.avail -= w;
+    return n1 + (k ? k : (one ? 1u : 0u));
+}
+
 // The resolve walk of chunk t (pass 0 with resolve, below): e = the pass-0 exit of chunk t - 1 (~0u: it
 // ended invalid), s0 = chunk t's pass-0 start, x0 = its pass-0 exit (window-relative), n = its pass-0
 // count, ex = its pass-0 exit (absolute).  On return n / exit are chunk t's true count and exit; true
@@ -599,6 +637,9 @@ __device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, u
 __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
     __shared__ uint32_t win[kSyncWinAlloc];
     __shared__ uint32_t s_exit[kEgBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kEgLutBits];
+    static_assert((1 << kEgLutBits) == 16 * kEgBlock, "one 16-byte piece per thread");
+    *(uint4*)(s_lut + 16 * threadIdx.x) = *(const uint4*)(kEgLut.e + 16 * threadIdx.x);  // ordered by the staging's barrier
     const bool rs = iteration == 0 && resolve;
     const uint64_t b = blockIdx.x;
     const uint64_t first = rs ? (b ? b * (kEgBlock - 1) - 1 : 0) : b * kEgBlock;
@@ -617,21 +658,18 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
     if (live) {
         r.seek(s0);
         // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary.
-        // The chunk interior first, without bounds (kLeanMargin), then the bounded steps to the chunk end,
-        // then the checked steps; a long or invalid code leaves the lean loops unconsumed.
-        // (the interior in the chunk's own coordinates, reading its column; lc: the chunk's index in the
-        // window -- threadIdx.x, but for block 0's resolving pass threadIdx.x - 1)
-        const uint32_t lc = (uint32_t)(t - first), cb = kChunkBits * lc;
-        const uint32_t fast_stop = stop > cb + kLeanMargin ? stop - cb - kLeanMargin : 0u;
+        // The chunk interior first, without bounds (kLeanMargin; by table: lean_step_lut), then the bounded
+        // steps to the chunk end, then the checked steps; a long or invalid code leaves the lean loops
+        // unconsumed.
+        const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
         // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
         // chunk end (a code running past the limit is invalid: the checked steps)
         const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
-        Lean c = lean_rebase(lean_from(r), -(int32_t)(16 * lc));
+        Lean c = lean_from(r);
         bool bad = false;
-        const ColRead col = col_of(win, lc);
-        while (!bad & (c.pos() < fast_stop)) n += lean_step2(col, c, bad);
-        c = lean_rebase(c, 16 * lc);
-        while (!bad & (c.pos() < bstop)) n += lean_step<true>(WinRead{win}, c, bad, bstop - c.pos());
+        const WinRead rd{win};
+        while (!bad & (c.pos() < fast_stop)) n += lean_step_lut(rd, s_lut, c, bad);
+        while (!bad & (c.pos() < bstop)) n += lean_step<true>(rd, c, bad, bstop - c.pos());
         lean_to(r, c);
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
         }
@@ -661,10 +699,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
 // the pass 708 -> 529 us on one box (round 4; stored one at a time as the parse reached them, through a
 // buffer descriptor, each lane's marks tens of microseconds apart, the lines were written back partial).
 // The slots cost 8.5 KiB per block (with the window, 6 blocks per CU instead of 8).  A step's one possible
-// mark is stored branch-free: steps without a mark store to the thread's dummy dword in an unused slot of
-// the window (row t / 16, column kEgBlock + 1 + t % 16; round 4: an 18th slot entry, which with the
-// transposed window's 2 KiB would have cost a block per CU; an exec-masked store instead of the dummy
-// compiled to a branch and 13 more VALU per step).
+// mark is stored branch-free: steps without a mark store to the thread's dummy, 2 bytes behind the
+// window (round 4: an 18th slot entry; an exec-masked store instead compiled to a branch and 13 more VALU
+// per step).
 // Marks leave as the low 32 bits of their bit position (round 5; 64-bit before: 0.52 GB written and read
 // back per c8 step), the whole position of every 64th (a consumer group's first) in mark_base.
 constexpr uint32_t kMkSlot = 17;  // a chunk has at most 17 marks (<= 512 values)
@@ -695,10 +732,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t sp = rel_bit(s, base);  // the chunk's true start (LDSM marks are relative to it)
     r.seek(sp);
     uint16_t* const myk = s_mk + threadIdx.x * kMkSlot;  // mark k of the chunk (value 32 k - ph) at myk[k]
-    // a step without a mark stores to the thread's dummy: half of a dword in an unused column (1 .. 16) of
-    // the slack rows (row threadIdx.x / 32)
-    uint16_t* const dummy = (uint16_t*)(win + kSlackRows + 32 * (threadIdx.x >> 5) + 1 + ((threadIdx.x & 31) >> 1)) +
-                            (threadIdx.x & 1);
+    uint16_t* const dummy = (uint16_t*)(win + kSyncWinWords) + threadIdx.x;  // a step without a mark stores here
     // chunk-relative 32-bit value count i (value idx0 + i): the 64-bit index arithmetic per step was a
     // large part of the pass.  A chunk holds at most ~kChunkBits + 64 codes, so rem below never binds
     // unless the wanted values end inside this chunk.
@@ -713,14 +747,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     // none of the bounds below can bind -- a lean loop without them (a long or invalid code leaves it for
     // the checked loop, which reads or reports it).
     const uint32_t lim_end = min(end, limit);
-    const uint32_t cb = kChunkBits * threadIdx.x;  // the chunk's first bit (the interior's coordinates)
-    const uint32_t fast_end = lim_end > cb + kLeanMargin ? lim_end - cb - kLeanMargin : 0u;
+    const uint32_t fast_end = lim_end > kLeanMargin ? lim_end - kLeanMargin : 0u;
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
     {
-        Lean c = lean_rebase(lean_from(r), -(int32_t)(16 * threadIdx.x));
+        Lean c = lean_from(r);
         bool bad = false;
-        const ColRead col = col_of(win, threadIdx.x);
-        const uint32_t spc = sp - cb;
+        const WinRead rd{win};
         // a step takes nv <= 32 values, value i + d at bit p0 + d: at most one mark, value i + d0
         auto mark = [&](uint32_t p0, uint32_t nv) {
             const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
@@ -732,19 +764,18 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
         while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
             const uint32_t p0 = c.pos();
             uint32_t n1, w;
-            const uint32_t nv = lean_step2<30u>(col, c, bad, &n1, &w);
+            const uint32_t nv = lean_step2<30u>(rd, c, bad, &n1, &w);
             const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
             const uint32_t at = p0 + d0 + (d0 > n1 ? w - 1u : 0u);
-            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(at - spc);  // no branch
+            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(at - sp);  // no branch
             i += nv;
         }
-        c = lean_rebase(c, 16 * threadIdx.x);
         // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
         // end take the checked steps)
         const uint32_t bend = limit >= end + 64u ? end : 0u;
         while (!bad & (c.pos() < bend) & (i < fast_rem)) {
             const uint32_t p0 = c.pos();
-            mark(p0, lean_step<true>(WinRead{win}, c, bad, bend - p0));
+            mark(p0, lean_step<true>(rd, c, bad, bend - p0));
         }
         lean_to(r, c);
     }
@@ -894,12 +925,18 @@ int launch_eg_scan(const EgParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, hipStream_t st) {
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, int segs_per_wave, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     if (launch_eg_scan(P, st)) return -1;
-    const uint64_t per = (uint64_t)kEgWaves * kCompactSPW;
+    const uint64_t per = (uint64_t)kEgWaves * (segs_per_wave == 8 ? 8 : 4);
     const uint64_t blocks = (P.n_cubes + per - 1) / per;
-    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
+#ifdef DCT3D_EG_COMPACT_PF4  // A/B only
+    constexpr int kPF8 = 4;
+#else
+    constexpr int kPF8 = 2;
+#endif
+    if (segs_per_wave == 8) hipLaunchKernelGGL((eg_compact_kernel<8, kPF8>), dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
+    else hipLaunchKernelGGL((eg_compact_kernel<4, 4>), dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
     hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -97,29 +97,9 @@ struct BitReader {
     }
 };
 
-// The block window of the sync and mark passes (dct3d_eg.hip): 256 chunks of 16 words, one per thread,
-// plus a slack chunk.  Word j of chunk c lives at dword (c >> 5) * 512 + 32 j + (c & 31) (round 5): each
-// group of 32 chunks is stored transposed, so the bank of a word (dword address mod 32 for ds_read_b32) is
-// its chunk mod 32 whatever j is, and the 32 lanes of a half-wave, each parsing its own chunk at its own
-// offset, read 32 distinct banks.  Linear (rounds 1-4), lane t started at word 16 t: banks 16 t mod 32,
-// two banks per half-wave, and with the offsets drifting apart ~7 extra LDS cycles per read
-// (tools/lds_bank_sim.py; the counters: 6.1 per LDS instruction).  The slack chunk (c = 256, 8 words)
-// takes column 0 of a ninth group.
-#ifdef DCT3D_EG_WIN_LINEAR  // A/B only: the rounds 1-4 layout
-constexpr uint32_t kColStride = 1;
-constexpr uint32_t kSlackRows = 256 * 16 + 8;  // the mark pass's dummies after the window
-__device__ __forceinline__ uint32_t win_at(uint32_t i) { return i; }
-__device__ __forceinline__ uint32_t col_base(uint32_t c) { return 16u * c; }
-#else
-constexpr uint32_t kColStride = 32;
-constexpr uint32_t kSlackRows = 256 * 16;  // the slack chunk's rows (column 0) and the mark pass's dummies
-__device__ __forceinline__ uint32_t win_at(uint32_t i) { return (i & ~511u) | ((i & 15u) << 5) | ((i >> 4) & 31u); }
-__device__ __forceinline__ uint32_t col_base(uint32_t c) { return (c >> 5) * 512u + (c & 31u); }
-#endif
-
 // The same reader over an LDS window with window-relative 32-bit positions (a window holds < 2^18
 // bits): the per-code 64-bit index, compare and carry arithmetic of absolute positions was most of the
-// parse's instructions.  Word i of the window is s[win_at(i)] (i < n), zero beyond.
+// parse's instructions.  Word i of the window is s[i] (i < n), zero beyond.
 struct WinReader {
     const uint32_t* s;
     uint32_t n;
@@ -130,7 +110,7 @@ struct WinReader {
     uint32_t pre;    // word `next` as read: zeroed past the window only where it is used, so that the
                      // LDS read's wait falls at the next refill, not right behind the read
     __device__ __forceinline__ uint32_t word(uint32_t i) const {
-        const uint32_t v = s[win_at(i < n ? i : 0u)];  // unconditional read
+        const uint32_t v = s[i < n ? i : 0u];  // unconditional read
         return i < n ? v : 0u;
     }
     __device__ __forceinline__ void seek(uint32_t p) {
@@ -140,14 +120,14 @@ struct WinReader {
         buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
         avail = 64 - sh;
         next = k + 2;
-        pre = s[win_at(next < n ? next : 0u)];
+        pre = s[next < n ? next : 0u];
     }
     __device__ __forceinline__ void refill() {
         if (avail <= 32) {
             buf |= (uint64_t)(next < n ? pre : 0u) << (32 - avail);
             avail += 32;
             ++next;
-            pre = s[win_at(next < n ? next : 0u)];
+            pre = s[next < n ? next : 0u];
         }
     }
     __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
