@@ -268,9 +268,8 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
 // eg_write_kernel.  (Round 4 before: lane-local words in slot columns and a lane bit-count array, the
 // lanes concatenated here through shuffles and an LDS image: 275 us per c7 step, 0.42 GB of slot reads;
 // one segment per wave: 201 us, two dependent round trips per 180 words.)
-// kCompactSPW segments per wave, kCompactPF rows of 64 words per segment per load round trip: 4 x 4
-// for 8x8x4's 8-cube segments, 8 x 2 for 8x8x8's 4-cube ones
-template <int kCompactSPW, int kCompactPF>
+constexpr int kCompactPF = 4;   // rows of 64 words per segment per load round trip
+constexpr int kCompactSPW = 4;  // segments per wave
 __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const uint32_t* __restrict__ slot,
                                                               uint32_t seg_cap) {
     if (P.status[1] != 0) return;  // capacity failure: nothing is written
@@ -509,6 +508,14 @@ __device__ __forceinline__ uint32_t lean_step(const Rd& s, Lean& c, bool& bad, u
 // avail < 64), so neither its bits nor its read reach the bound (nor, in chunk coordinates, word 15).
 constexpr uint32_t kLeanMargin = 128;
 static_assert(31 + 31 + 31 < kLeanMargin && 31 + 63 + 32 <= kLeanMargin, "lean steps stay inside the margin");
+// The margins the two interior loops use.  A step's reads past the bound stay inside the block window
+// (the last chunk's bound has the 256-bit slack behind it), so only the bits a step takes must stay short
+// of the bound: the table step of the sync pass takes <= 31 + 31 bits, the mark pass's two-code step
+// <= 30 + 31 + 31; the bounded steps then finish the chunk.
+// (128 for both, the window-read bound: sync 346 -> 311 us, mark 464 -> 442 us per c8 step, A/B x 3 on one
+// box, profiles/r05/c8_ab)
+constexpr uint32_t kSyncMargin = 64, kMarkMargin = 96;
+static_assert(31 + 31 < kSyncMargin && 30 + 31 + 31 < kMarkMargin && 31 * 8 < 256, "steps stay short of the bound");
 template <uint32_t CAP = 31u, class Rd>
 __device__ __forceinline__ uint32_t lean_step2(const Rd& s, Lean& c, bool& bad, uint32_t* n1_out = nullptr,
                                                uint32_t* w_out = nullptr) {
@@ -661,7 +668,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
         // The chunk interior first, without bounds (kLeanMargin; by table: lean_step_lut), then the bounded
         // steps to the chunk end, then the checked steps; a long or invalid code leaves the lean loops
         // unconsumed.
-        const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
+        const uint32_t fast_stop = stop > kSyncMargin ? stop - kSyncMargin : 0u;
         // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
         // chunk end (a code running past the limit is invalid: the checked steps)
         const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
@@ -747,7 +754,7 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     // none of the bounds below can bind -- a lean loop without them (a long or invalid code leaves it for
     // the checked loop, which reads or reports it).
     const uint32_t lim_end = min(end, limit);
-    const uint32_t fast_end = lim_end > kLeanMargin ? lim_end - kLeanMargin : 0u;
+    const uint32_t fast_end = lim_end > kMarkMargin ? lim_end - kMarkMargin : 0u;
     const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
     {
         Lean c = lean_from(r);
@@ -925,18 +932,12 @@ int launch_eg_scan(const EgParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, int segs_per_wave, hipStream_t st) {
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, hipStream_t st) {
     if (P.n_cubes == 0) return 0;
     if (launch_eg_scan(P, st)) return -1;
-    const uint64_t per = (uint64_t)kEgWaves * (segs_per_wave == 8 ? 8 : 4);
+    const uint64_t per = (uint64_t)kEgWaves * kCompactSPW;
     const uint64_t blocks = (P.n_cubes + per - 1) / per;
-#ifdef DCT3D_EG_COMPACT_PF4  // A/B only
-    constexpr int kPF8 = 4;
-#else
-    constexpr int kPF8 = 2;
-#endif
-    if (segs_per_wave == 8) hipLaunchKernelGGL((eg_compact_kernel<8, kPF8>), dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
-    else hipLaunchKernelGGL((eg_compact_kernel<4, 4>), dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
+    hipLaunchKernelGGL(eg_compact_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, slot, seg_cap);
     hipLaunchKernelGGL(eg_stitch_kernel, dim3((uint32_t)((P.n_cubes + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

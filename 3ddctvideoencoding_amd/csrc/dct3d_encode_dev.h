@@ -721,7 +721,6 @@ __device__ __forceinline__ void e16_flag_pos(uint32_t fm, int src, uint32_t cube
 // staged values are out of the registers by then).  s_b: the block's copy of the tables ([64] basis,
 // [32] thresholds), written by every wave that takes this path (identical bits) and read only after its
 // own writes.
-template <int S16C = kE16S16C, int S16F = kE16S16F>  // the int16 staging's cube and face strides
 __device__ __forceinline__ void e16_recheck64(const uint2 (&raw)[4], double bv, double tv, double* s_b, char* wl,
                                               int lane, uint32_t& fm, uint32_t& nset) {
     const int k = lane & 7, h = (lane >> 4) & 1;
@@ -772,7 +771,7 @@ __device__ __forceinline__ void e16_recheck64(const uint2 (&raw)[4], double bv, 
             const double n = __builtin_rint(q);
             if (__builtin_fabs(q - n) < s_b[64 + s]) {
                 const uint32_t cl = (lane >> 5) * 2 + ((lane & 15) >> 3);  // the cube within the wave
-                *(int16_t*)(wl + cl * S16C + kz * S16F + (ky * 8 + kx) * 2) = (int16_t)n;  // int16 staging
+                *(int16_t*)(wl + cl * kE16S16C + kz * kE16S16F + (ky * 8 + kx) * 2) = (int16_t)n;  // int16 staging
                 nset++;
             } else {
                 open |= 1u << bit;

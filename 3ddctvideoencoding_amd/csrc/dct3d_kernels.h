@@ -136,17 +136,10 @@ __device__ __forceinline__ uint64_t mark_at(const EgDecParams& P, uint64_t m, ui
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);
 int launch_encode_eg(int D, const EncodeParams& P, const EgFusedParams& E, hipStream_t st);
-// cubes per segment (one K1 wave) of the fused encode: 8x8x8 runs encode16_eg_kernel (4 cubes per wave,
-// 32 stream values per lane), 8x8x4 encode_eg_kernel<4> (8 cubes per wave, 32 values per lane)
-#ifdef DCT3D_EG_K1_OLD  // A/B only: encode_eg_kernel<8> (rounds 1-4)
-constexpr uint32_t eg_fused_cubes_per_segment(int D) { return 8u; }
-#else
-constexpr uint32_t eg_fused_cubes_per_segment(int D) { return D == 8 ? 4u : 8u; }
-#endif
 int launch_eg_stitch(const EgParams& P, hipStream_t st);
 // scan of the segment bits + the lanes' words concatenated into the stream + stitch (P.n_cubes =
 // segments, P.bits = seg_bits)
-int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, int segs_per_wave, hipStream_t st);
+int launch_eg_compact(const EgParams& P, const uint32_t* slot, uint32_t seg_cap, hipStream_t st);
 int launch_eg_encode(int D, const EgParams& P, hipStream_t st);
 // resolve (pass 0): each chunk's true parse is followed from the exit of chunk t - 1 until it meets a
 // pass-0 boundary of chunk t (in the block's LDS window); status[0] = 0: every chunk met, the pass-0 exits

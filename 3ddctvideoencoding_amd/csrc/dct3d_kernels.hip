@@ -315,140 +315,6 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
 }
 
 
-// Fused encode + Exp-Golomb, K1 at 8x8x8 (round 5): encode16_kernel's transform geometry -- 16 lanes per
-// cube, 4 cubes per wave, 72-VGPR transform (e16_body) -- instead of encode_eg_kernel<8>'s 8 lanes per
-// cube (64 floats per lane, 111 VGPRs: 4 waves per SIMD).  Segment = the wave's 4 cubes; lane (cp =
-// lane / 16, part = lane % 16) codes stream positions 32 part .. 32 part + 31 of cube cp.
-//   rows -> e16_body (statistics, passes X / Z / Y, quantise + certify, exact DC) -> int16 staging of
-//   the 4 cubes (encode16's layout) -> rare: the fp64 second certificate settles open coefficients in
-//   the staging, the exact Java fold what it leaves (exact ties), also into the staging -> the lane's
-//   32 values read from the staging in stream order (s_pos), mapped to their codes two at a time
-//   (eg_code_pair) -> eg_lane_emit.
-// The replay scratch (kMaxGroupsDev sums + products) has its own LDS: the staging holds the cubes until
-// the emission has read them.
-static_assert(kMaxGroupsDev * (4 + 8) % 16 == 0, "replay scratch alignment");
-// The int16 staging of encode16_eg_kernel: cube stride 1216 B (304 dwords, 16 mod 32: two cubes of a
-// half-wave on opposite bank halves), face stride 136 B (instead of encode16_kernel's 1152 / 144): the
-// emission's reads -- lane (cube, part) at diagonal position 32 part + i, 64 scattered 16-bit reads per
-// step -- 1.5 extra LDS cycles per read instead of 3.1 (host search over the strides), and the transform's
-// 8-byte staging stores without conflicts.  The emission read LDS-bound at 3.5 conflict cycles per LDS
-// instruction (SQ counters, round 5).
-constexpr int kEgS16C = 1216, kEgS16F = 136, kEgWaveLds = 4 * kEgS16C;
-static_assert(kEgWaveLds >= kE16Lds && 8 * kEgS16F <= kEgS16C, "the transform's region and the faces fit");
-template <int H>
-__device__ __forceinline__ uint32_t clz16(uint32_t x) {  // leading zeros of the zero-extended half H (32-bit count)
-    uint32_t z;
-    if constexpr (H == 0)
-        asm("v_ffbh_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(z) : "v"(x));
-    else
-        asm("v_ffbh_u32_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(z) : "v"(x));
-    return z;
-}
-__global__ __launch_bounds__(kBlock) void encode16_eg_kernel(EncodeParams P, EgFusedParams E) {
-    constexpr int CS = 512, VPL = 32;
-    constexpr int RS_B = kMaxGroupsDev * (4 + 8);
-    __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kEgWaveLds];
-    __shared__ __attribute__((aligned(16))) char s_rs[kWavesPerBlock * RS_B];
-    __shared__ __attribute__((aligned(16))) uint16_t s_pos[CS];  // stream position -> byte offset in a staged cube
-    __shared__ float4 s_tab[kTabN];
-    __shared__ double s_b64[96];  // second certificate tables (rare path)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = (xcd_tile<64>() * kWavesPerBlock + wave) * kE16CPW;
-    const uint32_t wid = cube0 / kE16CPW;  // segment index
-    const int k = lane & 7, h = (lane >> 4) & 1;
-    const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
-    const uint32_t g = cube0 + c;
-    const bool valid = g < P.n_cubes;
-    uint2 raw[4];
-    __builtin_amdgcn_s_setprio(3);  // loads ahead of the computing waves (encode16_kernel)
-    e16_load(P, g, valid, k, h, raw);
-    __builtin_amdgcn_s_setprio(0);
-    {  // diagonal position -> staging offset (kz * kEgS16F + (ky * 8 + kx) * 2), both loads in flight first
-        static_assert(CS % kBlock == 0, "whole passes");
-        uint16_t t[CS / kBlock];
-#pragma unroll
-        for (int r = 0; r < CS / kBlock; r++) t[r] = E.diag[threadIdx.x + r * kBlock];
-#pragma unroll
-        for (int r = 0; r < CS / kBlock; r++)
-            s_pos[threadIdx.x + r * kBlock] = (uint16_t)((t[r] >> 6) * kEgS16F + (t[r] & 63) * 2);
-    }
-    __syncthreads();
-    if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
-    char* wl = lds + wave * kEgWaveLds;
-    int32_t qv[8][4];
-    uint32_t fm = 0u;
-    enc_tables(P, s_tab, lane);
-    e16_body(P, raw, wl, s_tab, lane, valid, qv, fm);
-    {
-        char* dst = wl + c * kEgS16C + k * kEgS16F + h * 8;
-#pragma unroll
-        for (int ky = 0; ky < 8; ky++)
-            *(uint2*)(dst + ky * 16) = make_uint2(__builtin_amdgcn_perm(qv[ky][1], qv[ky][0], 0x05040100u),
-                                                  __builtin_amdgcn_perm(qv[ky][3], qv[ky][2], 0x05040100u));
-    }
-    wave_lds_sync();
-    if (__builtin_expect(__ballot(fm != 0u) != 0ull, 0)) {  // rare: open coefficients (wave-uniform)
-        if (P.recheck) {
-            uint2 raw2[4];
-            e16_load(P, g, valid, k, h, raw2);
-            const double bv = P.tab64[lane];
-            const double tv = lane < 32 ? P.tab64[64 + lane] : 0.0;
-            uint32_t nset;
-            e16_recheck64<kEgS16C, kEgS16F>(raw2, bv, tv, s_b64, wl, lane, fm, nset);
-        }
-        const ReplayGeom R{P.raster, P.cubes_per_stack, P.nbx, P.width, P.plane, P.stack_stride,
-                           E.ngroups, E.coef, E.group_of};
-        char* rs = s_rs + wave * RS_B;
-        for (;;) {
-            const uint64_t who = __ballot(fm != 0u);
-            if (who == 0ull) break;
-            const int src = (int)__builtin_ctzll(who);
-            uint32_t rg, rk;
-            e16_flag_pos(fm, src, cube0, rg, rk);
-            const int q = replay_fold<8, true>(replay_load<8>(R, rg, rk, lane), rk, lane, (int*)rs,
-                                               (double*)(rs + kMaxGroupsDev * 4));
-            if (lane == 0)
-                *(int16_t*)(wl + (rg - cube0) * kEgS16C + (rk >> 6) * kEgS16F + (rk & 63) * 2) = (int16_t)q;
-            if (lane == src) fm &= fm - 1u;
-            wave_lds_sync();
-        }
-    }
-
-#if defined(DCT3D_K1_SPLIT) && DCT3D_K1_SPLIT == 1  // DIAGNOSTIC timing split only: the transform part
-    if (lane == 0) E.seg_bits[wid] = 256u;  // a whole, in-bounds segment for the scan, compaction and stitch
-    return;
-#endif
-    // the lane's 32 values in stream order, as codes, two per register
-    const int cp = lane >> 4, part = lane & 15;
-    const bool lvalid = cube0 + cp < P.n_cubes;
-    const char* cb = wl + cp * kEgS16C;
-    uint32_t zs = 0;
-    uint32_t cds[VPL / 2];
-    if (lvalid) {
-#pragma unroll
-        for (int i0 = 0; i0 < VPL; i0 += 8) {
-            const uint4 pp = *(const uint4*)&s_pos[part * VPL + i0];
-            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
-#pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                const uint32_t lo = *(const uint16_t*)(cb + (pw[e >> 1] & 0xFFFFu));
-                const uint32_t hi = *(const uint16_t*)(cb + (pw[e >> 1] >> 16));
-                const uint32_t cc = eg_code_pair(hi, lo);
-                cds[(i0 + e) / 2] = cc;
-                zs += clz16<0>(cc) + clz16<1>(cc);
-            }
-        }
-    }
-#if defined(DCT3D_K1_SPLIT) && DCT3D_K1_SPLIT == 2  // DIAGNOSTIC timing split only: + the codes and widths
-    asm volatile("" ::"v"(zs));
-#pragma unroll
-    for (int i = 0; i < VPL / 2; i++) asm volatile("" ::"v"(cds[i]));
-    if (lane == 0) E.seg_bits[wid] = 256u;  // a whole, in-bounds segment for the scan, compaction and stitch
-    return;
-#endif
-    eg_lane_emit<VPL>(E, cds, zs, lvalid, lane, wid);
-}
-
 // =============================================================================================
 // Drop-in (A): float cube-major -> float cube-major, fp64 internal (3dDCT.cl:43-143 / 164-265)
 // =============================================================================================
@@ -767,12 +633,9 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
 namespace {
 template <int D>
 void launch_enc_eg_t(const EncodeParams& P, const EgFusedParams& E, hipStream_t st) {
-    const uint32_t cpw = eg_fused_cubes_per_segment(D);
-    const uint32_t groups = (P.n_cubes + cpw - 1) / cpw;
+    const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;
     const uint32_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    if constexpr (D == 8 && eg_fused_cubes_per_segment(8) == 4)
-        hipLaunchKernelGGL(encode16_eg_kernel, dim3(blocks), dim3(kBlock), 0, st, P, E);
-    else hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
+    hipLaunchKernelGGL((encode_eg_kernel<D>), dim3(blocks), dim3(kBlock), 0, st, P, E);
 }
 }  // namespace
 

@@ -818,10 +818,9 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (n_cubes == 0) return dct3d_eg_encode_dev(c, nullptr, 0, carry_byte, carry_bits, d_out, out_cap, total_bits);
     if (!d_out) return DCT3D_EINVAL;
     const int D = c->bd;
-    const uint32_t cps = eg_fused_cubes_per_segment(D), vpl = (uint32_t)c->plan.cs * cps / 64;
-    const uint64_t n_seg = (n_cubes + cps - 1) / cps, n_chunks = (n_seg + 4095) / 4096;
-    // worst case per lane: vpl values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 27 bits)
-    const uint32_t seg_cap = (uint32_t)(64 * ((vpl * 27 + 31) / 32));
+    const uint64_t n_seg = (n_cubes + 7) / 8, n_chunks = (n_seg + 4095) / 4096;
+    // worst case per lane: cs/8 values x 27 bits (|q| <= 255 sqrt(cs) -> codes <= 27 bits)
+    const uint32_t seg_cap = (uint32_t)(64 * (((c->plan.cs / 8) * 27 + 31) / 32));
     // two passes: K1 codes into per-segment slots, then scan + compaction (a single pass by decoupled
     // look-back wrote the same stream but measured slower: DESIGN.md §4b)
     if ((rc = c->d_egf_slot.grow(n_seg * seg_cap * sizeof(uint32_t))) ||
@@ -847,8 +846,6 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     P.tab_rstep = tabs;
     P.tab_G = tabs + kMaxS;
     P.tab_E = tabs + 2 * kMaxS;
-    P.tab64 = (const double*)c->d_tabs64.p;  // 8x8x8: the fp64 second certificate of encode16_eg_kernel
-    P.recheck = c->opt_enc_no_recheck ? 0u : 1u;
     EgFusedParams E;
     E.ngroups = (const int32_t*)c->d_ngroups.p;
     E.coef = (const double*)c->d_coef.p;
@@ -877,8 +874,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (launch_encode_eg(D, P, E, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[1], c->stream);
     if (ev) (void)hipEventRecord(ev[2], c->stream);
-    // 8x8x8's 4-cube segments (~90 words of ramp content) 8 per compaction wave, 8x8x4's 8-cube ones 4
-    if (launch_eg_compact(G, E.slot, seg_cap, cps == 4 ? 8 : 4, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_compact(G, E.slot, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
     if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
