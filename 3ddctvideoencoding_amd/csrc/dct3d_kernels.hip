@@ -290,6 +290,10 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
         }
     }
 
+#if defined(DCT3D_K1_SPLIT) && DCT3D_K1_SPLIT == 1  // DIAGNOSTIC timing split only: transform, staging, replays
+    if (lane == 0) E.seg_bits[wid] = 256u;  // a whole, in-bounds segment for the scan, compaction and stitch
+    return;
+#endif
     // Exp-Golomb: lane (cp, part) codes stream positions part*VPL .. +VPL-1 of cube cp (lane order =
     // stream order), read from the staged codes 8 at a time (eg_lane_emit)
     const int cp = lane >> 3, part = lane & 7;
@@ -311,6 +315,13 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
             }
         }
     }
+#if defined(DCT3D_K1_SPLIT) && DCT3D_K1_SPLIT == 2  // DIAGNOSTIC timing split only: + the codes and widths
+    asm volatile("" ::"v"(zs));
+#pragma unroll
+    for (int i = 0; i < VPL / 2; i++) asm volatile("" ::"v"(cds[i]));
+    if (lane == 0) E.seg_bits[wid] = 256u;
+    return;
+#endif
     eg_lane_emit<VPL>(E, cds, zs, lvalid, lane, wid);
 }
 
