@@ -136,3 +136,30 @@ def test_cli_decode_truncated_input_fails_cleanly(pkg, tmp_path, host_eg):
     r = subprocess.run([pkg.CLI_PATH, "decode", str(binf), str(outf), str(w), str(h), str(frames), "1"],
                        capture_output=True, text=True, env=env)
     assert r.returncode == 1 and "Truncated or corrupt" in r.stdout
+
+
+def test_cli_multi_device_distinct_gpus(pkg, plan8, tmp_path):
+    """encode_multi / decode_multi over two DISTINCT devices: one context, host thread and
+    per-device raster allocation on each GPU.  The round's boxes have one GPU, so this runs only where the
+    CLI lists two or more devices (the driver's 8-GPU node); elsewhere it skips."""
+    r = subprocess.run([pkg.CLI_PATH, "list_devices"], capture_output=True, text=True, timeout=120)
+    n_dev = sum(1 for line in r.stdout.splitlines() if " - HIP device " in line)
+    if n_dev < 2:
+        pytest.skip(f"{n_dev} HIP device(s): distinct-device multi-GPU codec needs two")
+    w, h, frames = 320, 240, 40
+    fr = pkg.synthetic.frames(w, h, frames, kind="ramp")
+    n_stacks = frames // 8
+    raw, b1, b2, o2 = tmp_path / "in.raw", tmp_path / "one.bin", tmp_path / "two.bin", tmp_path / "two.raw"
+    raw.write_bytes(fr.tobytes())
+    env = dict(os.environ, DCT3D_CODEC_BATCH="1")
+    for binf, dev in ((b1, "1"), (b2, "1,2")):
+        r = subprocess.run([pkg.CLI_PATH, "encode", str(raw), str(binf), str(w), str(h), str(frames), dev],
+                           capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+    assert b2.read_bytes() == b1.read_bytes()
+    r = subprocess.run([pkg.CLI_PATH, "decode", str(b2), str(o2), str(w), str(h), str(frames), "2,1"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    q = plan8.encode_q(fr)
+    dec = np.frombuffer(o2.read_bytes(), np.uint8).reshape(frames, h, w)
+    assert np.array_equal(dec, plan8.decode_q(q.reshape(-1, 8, 8, 8), w, h, frames))
