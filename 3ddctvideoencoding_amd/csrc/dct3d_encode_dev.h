@@ -804,7 +804,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     __shared__ float4 s_tab[kTabN];
     __shared__ double s_b64[96];  // second certificate tables (rare path)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t cube0 = P.g_base + (xcd_tile<64>() * kWavesPerBlock + wave) * kE16CPW;
+#ifndef DCT3D_E16_XCD_G  // A/B only: the XCD tile run length of encode16_kernel
+#define DCT3D_E16_XCD_G 64
+#endif
+    const uint32_t cube0 = P.g_base + (xcd_tile<DCT3D_E16_XCD_G>() * kWavesPerBlock + wave) * kE16CPW;
     const int k = lane & 7, h = (lane >> 4) & 1;
     const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
     const uint32_t g = cube0 + c;
