@@ -97,9 +97,11 @@ def parse():
                     help="N>1, encode configs: also time the optional host-of-record distribution (SURVEY.md §8e): "
                          "rank 0 scatters every rank's u8 stacks and gathers the int32 cubes back over RCCL p2p "
                          "(reported under 'xgmi', never part of 'value')")
-    ap.add_argument("--settle-ms", type=float, default=150.0,
+    ap.add_argument("--settle-ms", type=float, default=4000.0,
                     help="untimed steps for at least this much wall time before the warmup steps (the GPU's "
-                         "power-management transient, ~30 ms of load); 0 = off")
+                         "power-management transient, ~30 ms of load; 4 s so that a sampler of GPU activity "
+                         "polling every few seconds sees the run: 150 vs 3000 ms measured the same c2 "
+                         "line, profiles/r05/settle/); 0 = off")
     ap.add_argument("--kernel-events", default="separate", choices=["separate", "timed"],
                     help="where the library's per-launch events (kernel_ms) run: a separate pass after the timed "
                          "region (default) or inside it (adds their device cost to every step)")
