@@ -307,7 +307,11 @@ __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, 
 // once the staged input is in registers (the persistent variant issues the next tile's loads there);
 // reload(g, cf, lane) re-reads cube g's dequantised coefficients for the rare exact replay.
 // PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
-template <int D, int PG, bool LOOP = false, class AfterA, class Reload>
+// CODES: the staging holds Exp-Golomb codes, not values (decode_eg_kernel): v = code >> 1, negative when the
+// code is odd -- the sign goes into the converted magnitude's sign bit (one v_lshl_or) and the product is the same exact
+// q * step, except that code 1 (value 0) gives -0.0 (|cf| in L1, and the outputs' truncation and
+// certificate, do not see a zero's sign; the exact replay reloads the values).
+template <int D, int PG, bool LOOP = false, bool CODES = false, class AfterA, class Reload>
 __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
                                             AfterA&& after_a, const Reload& reload) {
     using G = DecGeom<D>;
@@ -344,7 +348,14 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
             const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                b[ky][e] = __dmul_rn((double)vv[e], stp[e + ky]);
+                if constexpr (CODES) {
+                    const uint32_t cd = (uint32_t)vv[e];
+                    uint2 m = __builtin_bit_cast(uint2, (double)(cd >> 1));
+                    asm("v_lshl_or_b32 %0, %1, 31, %2" : "=v"(m.y) : "v"(cd), "v"(m.y));  // (the compiler: 2 VALU)
+                    b[ky][e] = __dmul_rn(__builtin_bit_cast(double, m), stp[e + ky]);
+                } else {
+                    b[ky][e] = __dmul_rn((double)vv[e], stp[e + ky]);
+                }
                 l1 = __dadd_rn(l1, __builtin_fabs(b[ky][e]));
             }
         }

@@ -811,6 +811,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
             atomicOr((unsigned int*)&P.status[2], (uint64_t)p1 + 32 <= limit && r.pos <= limit ? 1u : 2u);
             return;
         }
+        // a code of 33+ bits (|v| >= 2^15): the consumers' parse steps check for them (parse_step CHECK).
+        // Every code of the wanted values is parsed here or in the lean loops above, which leave every
+        // such code to this loop.
+        if (code >= 0x10000u) atomicOr((unsigned int*)&P.status[3], 1u);
         if (((ph + i) & (kMarkVals - 1)) == 0) myk[(ph + i) / kMarkVals] = (uint16_t)(p1 - sp);
         if (++i == rem && ends_here) P.status[1] = base + r.pos;
     }
@@ -864,15 +868,15 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int32_t v[kMarkVals];
-    parse_values<kMarkVals>(P, win, nwin, w0, fits, my, v);
+    uint32_t v[kMarkVals];
+    parse_codes<kMarkVals>(P, win, nwin, w0, fits, P.status[3] != 0, my, v);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint32_t c = lane / PARTS, part = lane % PARTS;
     int32_t* st = (int32_t*)wl + c * CS;
 #pragma unroll
-    for (uint32_t i = 0; i < kMarkVals; i++) st[s_diag[part * kMarkVals + i]] = v[i];
+    for (uint32_t i = 0; i < kMarkVals; i++) st[s_diag[part * kMarkVals + i]] = eg_value_fast(v[i]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -179,11 +179,12 @@ __device__ __forceinline__ int32_t eg_value(uint32_t code) {  // ExpGolombReader
     return (m & 1u) ? (int32_t)((m + 1u) >> 1) : -(int32_t)(m >> 1);
 }
 
-// 31 - 2 z (32 - the width of a code with z leading zeros) as one v_mad_i32_i24 (the compiler would emit
-// a shift and a subtract)
-__device__ __forceinline__ uint32_t eg_rshift(uint32_t z) {
-    uint32_t r;
-    asm("v_mad_i32_i24 %0, %1, -2, 31" : "=v"(r) : "v"(z));
+// minus the width of a code with z leading zeros, -(2 z + 1), as one v_mad_i32_i24.  Its low 5 bits are
+// 32 - the width: the shift amount of v_lshrrev / v_alignbit (which read only those bits) that takes the
+// code off the top of a 32-bit window, and the sum of a step's values is minus the bits it took.
+__device__ __forceinline__ int32_t eg_negwidth(uint32_t z) {
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, -2, -1" : "=v"(r) : "v"(z));
     return r;
 }
 
@@ -202,74 +203,88 @@ __device__ __forceinline__ uint32_t win_code_at(const uint32_t* win, uint32_t& q
 // and C codes of <= 31 bits (|v| < 2^15: every code an encoder of 8-bit frames writes) take at most 31 C
 // of them.  No buffer is carried between steps, so no refill test and no divergent refill branch: a step
 // is one round of LDS reads, C funnel shifts, and per code a leading-zero count, a shift and the funnel
-// shifts of the bits behind it.  A longer code (wave-uniform test) re-reads the step's codes at their
-// positions.  win[-1] must be readable (the window starts one word into its region): it is read, and
-// ignored, at p = 0.
-template <int C>
-__device__ __forceinline__ void parse_step(const uint32_t* win, uint32_t& p, uint32_t (&code)[C]) {
-    const uint32_t* w = win + ((p + 31u) >> 5);
-    const uint32_t s = 0u - p;  // the funnel shift's low 5 bits: (32 - p mod 32) mod 32
-    uint32_t x[C + 1], b[C], sh[C];
+// shifts of the bits behind it.  win[-1] must be readable (the window starts one word into its region):
+// it is read, and ignored, at p = 0.
+// The position is carried negated, n = -p: the funnel shift (32 - p mod 32) mod 32 is n's low 5 bits
+// (alignbit reads no others), k = -(n >> 5) (arithmetic shift), and n moves by the codes' negated widths
+// (eg_negwidth), which are their shift amounts too -- the step's address is a shift and an add, its
+// position update two three-operand adds (round 5: p's ceiling, shift and update were 9 VALU of ~34).
+// CHECK: a code of 33+ bits may occur (the mark pass saw one: status[3]); the step's codes are then
+// re-read at their positions when one of them is that long (wave-uniform test).  Otherwise no code is.
+template <int C, bool CHECK>
+__device__ __forceinline__ void parse_step(const uint32_t* win, int32_t& n, uint32_t (&code)[C]) {
+    const uint32_t* w = (const uint32_t*)((const char*)win + __mul24(n >> 5, -4));
+    const uint32_t s = (uint32_t)n;
+    uint32_t x[C + 1], b[C];
+    int32_t nw[C];
 #pragma unroll
     for (int j = 0; j <= C; j++) x[j] = w[j - 1];
 #pragma unroll
     for (int j = 0; j < C; j++) b[j] = __builtin_amdgcn_alignbit(x[j], x[j + 1], s);
-    uint32_t mn = 0xFFFFFFFFu, sum = 0;
+    uint32_t mn = 0xFFFFFFFFu;
 #pragma unroll
     for (int e = 0; e < C; e++) {
-        sh[e] = eg_rshift(__builtin_clz(b[0]));  // 32 - the code's width
-        code[e] = b[0] >> sh[e];
-        mn = min(mn, b[0]);
-        sum += sh[e];
+        nw[e] = eg_negwidth(__builtin_clz(b[0]));
+        code[e] = b[0] >> (uint32_t)nw[e];
+        if constexpr (CHECK) mn = min(mn, b[0]);
 #pragma unroll
-        for (int j = 0; j + 1 < C - e; j++) b[j] = __builtin_amdgcn_alignbit(b[j], b[j + 1], sh[e]);
+        for (int j = 0; j + 1 < C - e; j++) b[j] = __builtin_amdgcn_alignbit(b[j], b[j + 1], (uint32_t)nw[e]);
     }
-    if (__builtin_expect(__ballot(mn < 0x10000u) != 0ull, 0)) {  // a code of 33+ bits
+    int32_t sum = 0;
+#pragma unroll
+    for (int e = 0; e < C; e++) sum += nw[e];
+    if (CHECK && __builtin_expect(__ballot(mn < 0x10000u) != 0ull, 0)) {  // a code of 33+ bits
+        uint32_t p = (uint32_t)-n;
 #pragma unroll
         for (int e = 0; e < C; e++) code[e] = win_code_at(win, p);
+        n = -(int32_t)p;
     } else {
-        p += 32u * C - sum;
+        n += sum;
     }
 }
 
-// A consumer lane's N values from window bit p: four codes per step (the window carries 5 words of slack
-// past the last mark: a step reads up to word ceil(p / 32) + 3)
-template <int N>
-__device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, int32_t (&v)[N]) {
+// A consumer lane's N codes from window bit p: four per step (the window carries 5 words of slack past
+// the last mark: a step reads up to word ceil(p / 32) + 3)
+template <int N, bool CHECK>
+__device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, uint32_t (&cd)[N]) {
     static_assert(N % 4 == 0, "steps of four");
+    int32_t n = -(int32_t)p;
 #pragma unroll
     for (int i = 0; i < N; i += 4) {
         uint32_t c[4];
-        parse_step<4>(win, p, c);
+        parse_step<4, CHECK>(win, n, c);
 #pragma unroll
-        for (int e = 0; e < 4; e++) v[i + e] = eg_value_fast(c[e]);
+        for (int e = 0; e < 4; e++) cd[i + e] = c[e];
     }
 }
 
-// A consumer lane's N values from stream bit `my` (a mark: the stream is validated by the mark pass).
-// fits (wave-uniform): the wave's bit range is staged in its LDS window (words [w0, w0 + nwin), win[-1]
-// readable: parse_step); else
-// the parse reads the stream in global memory -- a wave whose 2,048 values average more than the window
-// holds (|q| >= 2^13 nearly everywhere: never written by an encoder of 8-bit frames, but a valid stream).
-// That path's values pass through the (then unused) window region, lane-private rows of N words (64 N
-// words: every caller's region holds them), so that v is written at constant indices only (a runtime index into v would make a caller's loop carry
-// all of v: decode_eg_kernel).
+// A consumer lane's N codes (not values: eg_value_fast, or the decode's dequantisation, converts) from
+// stream bit `my` (a mark: the stream is validated by the mark pass).  long_codes (status[3], grid-uniform):
+// the stream holds a code of 33+ bits.  fits (wave-uniform): the wave's bit range is staged in its LDS
+// window (words [w0, w0 + nwin), win[-1] readable: parse_step); else the parse reads the stream in global
+// memory -- a wave whose 2,048 values average more than the window holds (|q| >= 2^13 nearly everywhere:
+// never written by an encoder of 8-bit frames, but a valid stream).  That path's codes pass through the
+// (then unused) window region, lane-private rows of N words (64 N words: every caller's region holds
+// them), so that cd is written at constant indices only (a runtime index into cd would make a caller's
+// loop carry all of cd: decode_eg_kernel).
 template <int N>
-__device__ __forceinline__ void parse_values(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
-                                             bool fits, uint64_t my, int32_t (&v)[N]) {
+__device__ __forceinline__ void parse_codes(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
+                                            bool fits, bool long_codes, uint64_t my, uint32_t (&cd)[N]) {
     if (fits) {
-        parse_win<N>(win, my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u, v);
+        const uint32_t p = my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u;
+        if (long_codes) parse_win<N, true>(win, p, cd);
+        else parse_win<N, false>(win, p, cd);
     } else {
-        int32_t* row = (int32_t*)(win - 1) + (threadIdx.x & 63) * N;  // from the region's first word
+        uint32_t* row = (win - 1) + (threadIdx.x & 63) * N;  // from the region's first word
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
         r.seek(my);
         for (int i = 0; i < N; i++) {
             uint32_t code = 1u;
             (void)r.get(code);
-            row[i] = eg_value(code);
+            row[i] = code;
         }
 #pragma unroll
-        for (int i = 0; i < N; i++) v[i] = row[i];
+        for (int i = 0; i < N; i++) cd[i] = row[i];
     }
 }
 

@@ -520,6 +520,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     dec_clear_next_slot(P);
     // corrupt / short / empty stream: reported by the mark pass (block-uniform)
     if (E.status[2] != 0 || E.n_words == 0) return;
+    const bool long_codes = E.status[3] != 0;  // the stream holds a code of 33+ bits (the mark pass)
     {  // both loads in flight before the LDS writes
         static_assert(CS % kBlock == 0, "whole passes");
         uint16_t t[CS / kBlock];
@@ -606,8 +607,8 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         uint32_t myl_n = 0;
         if (i + 1 < NG) load_marks(lane, cube_of(i + 1), gb_n, myl_n, last_n);  // in flight during the parse
         wave_lds_sync();
-        int32_t v[32];
-        parse_values<32>(E, win, nwin, w0, fits, w0 * 32 + rel, v);
+        uint32_t v[32];  // codes: decode_tile<CODES> converts them in its dequantisation
+        parse_codes<32>(E, win, nwin, w0, fits, long_codes, w0 * 32 + rel, v);
         if (i + 1 < NG) open_window(lane, gb_n, myl_n, last_n, w0, rel, span, pw);  // in flight during the transform
         wave_lds_sync();
         {  // each value to its diagonal position in the staging: 8 offsets per 16-byte table read
@@ -620,11 +621,11 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
                 const uint32_t w[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
                 for (int e = 0; e < 8; e++)
-                    *(int32_t*)(cb + ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu)) = v[q * 8 + e];
+                    *(uint32_t*)(cb + ((w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu)) = v[q * 8 + e];
             }
         }
         wave_lds_sync();
-        decode_tile<D, 1, (NG > 1)>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, E.mark_base, s_diag});
+        decode_tile<D, 1, (NG > 1), true>(P, wl, lane, cube0, [] {}, ReloadStream<D>{E.words, E.n_words, E.mark, E.mark_base, s_diag});
         // the region receives the next group's window: after a block store (its rows are read by every
         // wave of the block) the whole block must be past it (block-uniform condition, as dec_store_tile's)
         if (i + 1 < NG) {

@@ -263,6 +263,43 @@ def test_fused_decode_dense_long_codes(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_
     assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
 
 
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("with_long", [False, True])
+def test_fused_decode_sparse_long_codes(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, with_long):
+    """The consumer's parse steps take codes of <= 31 bits unchecked unless the mark pass saw a longer one
+    (status[3]): a few 33..41-bit codes (|q| = 2^15 .. 2^20) among ordinary values, in windows that fit
+    the LDS, flag the stream and are parsed by the checking steps; |q| = 2^15 - 1 (31 bits, the widest
+    code of the unchecked steps) is parsed by either.  Both give the Java-semantics raster."""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    rng = np.random.default_rng(21 + depth + 2 * with_long)
+    n = ctx.n_cubes(256, 128, 2)
+    q = rng.integers(-20, 21, size=(n, depth, 8, 8))
+    q[rng.random(q.shape) < 0.5] = 0
+    sgn = rng.choice([-1, 1], size=q.shape)
+    edge = rng.random(q.shape) < 0.002
+    q[edge] = (2**15 - 1) * sgn[edge]
+    if with_long:
+        big = rng.random(q.shape) < 0.001
+        q[big] = rng.integers(2**15, 2**20, size=int(big.sum())) * sgn[big]
+        q[0, 0, 0, 0] = 2**15  # the narrowest long code, 33 bits
+    q = q.astype(np.int32)
+    data, nbits = _expected(oracle, pkg, q, depth)
+    got, eb = _decode_fused(ctx, data, 256, 128, 2)
+    assert eb == nbits
+    assert np.array_equal(got, plan.decode_q(q, 256, 128, 2 * depth))
+    qd, eb2 = _eg_decode_q(ctx, data, n)  # the stream -> int32 path (eg_emit_kernel) parses the same way
+    assert eb2 == nbits and np.array_equal(qd, q)
+
+
+def _eg_decode_q(ctx, data: bytes, n_cubes: int):
+    import torch
+    d = _stream_dev(data)
+    dq = torch.zeros(n_cubes * ctx.cube_size, dtype=torch.int32, device="cuda")
+    eb = ctx.eg_decode_dev(d, len(data), 0, n_cubes, dq)
+    ctx.synchronize()
+    return dq.cpu().numpy().reshape(n_cubes, ctx.bd, 8, 8), eb
+
+
 def test_speculative_front_rerun_on_unresolved_pass0(pkg, oracle, plan8, gpu_ctx8):
     """The stream decode enqueues its scan, mark pass and consumer right behind the resolving sync pass
     (no host round trip); should pass 0 not resolve, the mark pass writes nothing, the consumer skips
