@@ -245,16 +245,20 @@ __device__ __forceinline__ void parse_step(const uint32_t* win, int32_t& n, uint
 
 // A consumer lane's N codes from window bit p: four per step (the window carries 5 words of slack past
 // the last mark: a step reads up to word ceil(p / 32) + 3)
+#ifndef DCT3D_PARSE_C
+#define DCT3D_PARSE_C 4
+#endif
 template <int N, bool CHECK>
 __device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, uint32_t (&cd)[N]) {
-    static_assert(N % 4 == 0, "steps of four");
+    constexpr int C = DCT3D_PARSE_C;
+    static_assert(N % C == 0, "whole steps");
     int32_t n = -(int32_t)p;
 #pragma unroll
-    for (int i = 0; i < N; i += 4) {
-        uint32_t c[4];
-        parse_step<4, CHECK>(win, n, c);
+    for (int i = 0; i < N; i += C) {
+        uint32_t c[C];
+        parse_step<C, CHECK>(win, n, c);
 #pragma unroll
-        for (int e = 0; e < 4; e++) cd[i + e] = c[e];
+        for (int e = 0; e < C; e++) cd[i + e] = c[e];
     }
 }
 

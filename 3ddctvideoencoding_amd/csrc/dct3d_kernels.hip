@@ -563,8 +563,12 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         rel = d < (1ull << 20) ? (uint32_t)d : 0u;
         const uint64_t lw = uniform_u64(last);
         span = (lw >> 5) + 5 - w0;
+        // word w0 + j from a scalar base, j clamped into the stream in 32 bits (a look-ahead past the last
+        // group reads a w0 made of other data: clamped too)
+        const uint64_t wb = min(w0, E.n_words - 1);
+        const uint32_t jmax = (uint32_t)min(E.n_words - 1 - wb, (uint64_t)0xFFFFFFFFu);
 #pragma unroll
-        for (int b = 0; b < NWP; b++) t[b] = E.words[min(w0 + (uint64_t)(b * 64 + lane), E.n_words - 1)];
+        for (int b = 0; b < NWP; b++) t[b] = E.words[wb + min((uint32_t)(b * 64 + lane), jmax)];
     };
     uint64_t w0, span;
     uint32_t rel;
@@ -584,12 +588,17 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         // the transform (which needs the registers)
         int lane = lane0;
         asm volatile("" : "+v"(lane));
-        const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_values)
+        const bool fits = span <= WIN;  // wave-uniform; else the parse reads global memory (parse_codes)
         const uint32_t nwin = (uint32_t)(fits ? span : 0);
+        // window words past the stream's end read as zero (w0 < n_words: the group's first mark is in it)
+        const uint32_t nlive = (uint32_t)min((uint64_t)nwin, E.n_words - w0);
+        // the look-ahead words, in rows of 64 (a wave-uniform test per row, no per-lane branch: the region
+        // holds NWP * 64 words, and those past the window are never read)
+        static_assert(NWP * 64 <= WIN, "look-ahead inside the region");
 #pragma unroll
         for (int b = 0; b < NWP; b++) {
             const uint32_t j = b * 64 + lane;
-            if (j < nwin) win[j] = w0 + j < E.n_words ? __builtin_bswap32(pw[b]) : 0u;
+            if (b * 64 < nwin) win[j] = j < nlive ? __builtin_bswap32(pw[b]) : 0u;
         }
         // the rest of a window longer than the look-ahead (content above 4 bits per value): 4 words per
         // lane per round, all loads issued before the first LDS write
@@ -600,7 +609,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
 #pragma unroll
             for (int b = 0; b < 4; b++) {
                 const uint32_t j = i0 + b * 64 + lane;
-                if (j < nwin) win[j] = w0 + j < E.n_words ? __builtin_bswap32(t[b]) : 0u;
+                if (j < nwin) win[j] = j < nlive ? __builtin_bswap32(t[b]) : 0u;
             }
         }
         uint64_t gb_n = 0, last_n = 0;
