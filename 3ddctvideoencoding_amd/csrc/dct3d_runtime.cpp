@@ -26,6 +26,10 @@ using namespace dct3d;
 
 namespace {
 
+// the stream decode's status words (d_egd_status): [0, 4) the sync / mark passes' (EgDecParams::status),
+// [4, 6) the chunk scan's (EgParams::status)
+constexpr size_t kEgdStatusBytes = 6 * sizeof(uint64_t);
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -89,7 +93,10 @@ struct dct3d_ctx {
     // fused encode + Exp-Golomb: per-segment slots and lane bit counts
     DevBuf d_egf_slot;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
+    // (d_egd_status: the decode's four status words, then the scan's two -- one read-back per call)
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
+    // pinned host words the entropy stages' status lands in (one DMA read-back, not a pageable copy)
+    uint64_t* h_status = nullptr;
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
     hipStream_t s_up = nullptr, s_down = nullptr;
     hipEvent_t pe_in[2] = {}, pe_done[2] = {};
@@ -140,6 +147,16 @@ const char* dct3d_strerror(int code) {
         case DCT3D_ENODATA: return "input stream ends early";
         default: return "unknown error";
     }
+}
+
+// the status words of an entropy stage (device, written by its kernels on the context stream): one
+// asynchronous copy into the pinned words, then the stream's completion
+static int read_status(dct3d_ctx* c, const void* d_status, size_t bytes, uint64_t* out) {
+    if (hipMemcpyAsync(c->h_status, d_status, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return DCT3D_EDEVICE;
+    memcpy(out, c->h_status, bytes);
+    return DCT3D_OK;
 }
 
 static int upload(DevBuf& b, const void* src, size_t bytes) {
@@ -230,7 +247,11 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         rc = upload(c->d_diag, diag.data(), diag.size() * sizeof(uint16_t));
     }
     if (!rc) rc = c->d_eg_status.grow(16);
-    if (!rc) rc = c->d_egd_status.grow(32);
+    if (!rc) rc = c->d_egd_status.grow(kEgdStatusBytes);
+    if (!rc && hipHostMalloc((void**)&c->h_status, kEgdStatusBytes, hipHostMallocDefault) != hipSuccess) {
+        c->h_status = nullptr;
+        rc = DCT3D_ENOMEM;
+    }
     if (rc) {
         dct3d_ctx_destroy(c);
         return rc;
@@ -249,6 +270,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
                       &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egd_mark,
                       &c->d_egf_slot})
         b->release();
+    if (c->h_status) (void)hipHostFree(c->h_status);
     for (auto& q : c->ev)
         for (auto& e : q)
             if (e) (void)hipEventDestroy(e);
@@ -780,9 +802,7 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     P.carry_byte = carry_byte;
     if (launch_eg_encode(c->bd, P, c->stream)) return DCT3D_EKERNEL;
     uint64_t st[2] = {0, 0};
-    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return DCT3D_EDEVICE;
+    if (read_status(c, c->d_eg_status.p, 16, st)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     if (st[1] & 2) return DCT3D_EINVAL;
     if (st[1] & 1) return DCT3D_ENOSPC;
@@ -876,9 +896,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (launch_eg_compact(G, E.slot, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
-    if (hipMemcpyAsync(st, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return DCT3D_EDEVICE;
+    if (read_status(c, c->d_eg_status.p, 16, st)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     if (st[1] & 1) return DCT3D_ENOSPC;
@@ -985,7 +1003,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     const bool resolve = !c->opt_eg_no_resolve;
     int cur = 0;
     for (uint64_t it = 0; it <= n_chunks + 1; it++) {
-        if (hipMemsetAsync(c->d_egd_status.p, 0, 32, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+        if (hipMemsetAsync(c->d_egd_status.p, 0, kEgdStatusBytes, c->stream) != hipSuccess) return DCT3D_EDEVICE;
         D.exit_in = ex[cur];
         D.exit_out = ex[cur ^ 1];
         if (launch_eg_sync(D, (int)(it < 2 ? it : 1), resolve, c->stream)) return DCT3D_EKERNEL;
@@ -998,9 +1016,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
             break;
         }
         uint64_t changed = 0;
-        if (hipMemcpyAsync(&changed, c->d_egd_status.p, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipStreamSynchronize(c->stream) != hipSuccess)
-            return DCT3D_EDEVICE;
+        if (read_status(c, c->d_egd_status.p, 8, &changed)) return DCT3D_EDEVICE;
         if (!changed) break;
         if (it == n_chunks + 1) return DCT3D_EINVAL;  // cannot happen: every pass fixes one more chunk
     }
@@ -1011,9 +1027,8 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     S.bits = D.count;
     S.off = D.off;
     S.bsum = (uint64_t*)c->d_eg_bsum.p;
-    S.status = (uint64_t*)c->d_eg_status.p;
+    S.status = D.status + 4;  // zeroed with the decode's words
     S.out_cap_words = ~0ull;
-    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
     if (launch_eg_mark(D, c->stream)) return DCT3D_EKERNEL;
@@ -1022,11 +1037,10 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
 
 // waits for the stream; the decode's verdict (corrupt: EINVAL, too short: ENODATA) and end bit
 static int eg_decode_status(dct3d_ctx* c, const EgDecParams& D, uint64_t* end_bit) {
-    uint64_t st[4] = {0, 0, 0, 0}, total[2] = {0, 0};
-    if (hipMemcpyAsync(st, c->d_egd_status.p, 32, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipMemcpyAsync(total, c->d_eg_status.p, 16, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return DCT3D_EDEVICE;
+    uint64_t w[6] = {0, 0, 0, 0, 0, 0};
+    if (read_status(c, c->d_egd_status.p, kEgdStatusBytes, w)) return DCT3D_EDEVICE;
+    const uint64_t* st = w;         // the decode's words
+    const uint64_t* total = w + 4;  // the scan's: total bits, flags
     if (st[2] & 4) return kEgRetry;  // a speculative front whose pass 0 did not resolve: rerun
     if (st[2] & 1) return DCT3D_EINVAL;
     if ((st[2] & 2) || total[0] < D.n_values) return DCT3D_ENODATA;
