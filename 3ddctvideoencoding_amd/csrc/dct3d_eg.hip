@@ -465,8 +465,7 @@ struct WinRead {
 // short by avail takes no code; the next step continues it.  BOUNDED: room (>= 1) bits are left before
 // the parse's stop; the run ends there at the latest and a code is taken only if it starts before it,
 // so the parse ends exactly at the first code boundary at or past the stop (the code may reach past).
-// CAP: the run's cap when unbounded (31; the mark pass's two-code step: 30, so that a step takes <= 32
-// values).  n1_out / w_out: the run's length and the code's width (0: none).
+// CAP: the run's cap when unbounded (31).  n1_out / w_out: the run's length and the code's width (0: none).
 template <bool BOUNDED = false, uint32_t CAP = 31u, class Rd>
 __device__ __forceinline__ uint32_t lean_step(const Rd& s, Lean& c, bool& bad, uint32_t room = 32u,
                                               uint32_t* n1_out = nullptr, uint32_t* w_out = nullptr) {
@@ -500,55 +499,39 @@ __device__ __forceinline__ uint32_t lean_step(const Rd& s, Lean& c, bool& bad, u
     if (w_out) *w_out = w;
     return n1 + (take ? 1u : 0u);
 }
-// lean_step, then a second code when it lies wholly in the buffered bits (no refill between): dense
-// content (few 1-bit codes, the steps mostly a run of 0-1 and one code) takes two codes per step.  A step
-// moves at most CAP + 31 + 31 bits and CAP + 2 values; the second code starts at bit n1 + w of the step.
-// The interior loops run while the parse is kLeanMargin bits short of every bound: a step then moves at
-// most 93 bits and reads the word that starts at most 31 + 63 bits past its position (the refill leaves
-// avail < 64), so neither its bits nor its read reach the bound (nor, in chunk coordinates, word 15).
-constexpr uint32_t kLeanMargin = 128;
-static_assert(31 + 31 + 31 < kLeanMargin && 31 + 63 + 32 <= kLeanMargin, "lean steps stay inside the margin");
-// The margins the two interior loops use.  A step's reads past the bound stay inside the block window
-// (the last chunk's bound has the 256-bit slack behind it), so only the bits a step takes must stay short
-// of the bound: the table step of the sync pass takes <= 31 + 31 bits, the mark pass's two-code step
-// <= 30 + 31 + 31; the bounded steps then finish the chunk.
-// (128 for both, the window-read bound: sync 346 -> 311 us, mark 464 -> 442 us per c8 step, A/B x 3 on one
-// box, profiles/r05/c8_ab)
-constexpr uint32_t kSyncMargin = 64, kMarkMargin = 96;
-static_assert(31 + 31 < kSyncMargin && 30 + 31 + 31 < kMarkMargin && 31 * 8 < 256, "steps stay short of the bound");
-template <uint32_t CAP = 31u, class Rd>
-__device__ __forceinline__ uint32_t lean_step2(const Rd& s, Lean& c, bool& bad, uint32_t* n1_out = nullptr,
-                                               uint32_t* w_out = nullptr) {
-    const uint32_t n = lean_step<false, CAP, Rd>(s, c, bad, 32u, n1_out, w_out);
-    // bits past avail are zero: a code whose leading zeros run past them is not taken (w2 > avail)
-    const uint32_t z2 = (uint32_t)__builtin_clz(c.hi | 1u);
-    const uint32_t w2 = 2u * z2 + 1u;
-    const bool take2 = !bad && z2 < 16u && w2 <= c.avail;
-    const uint32_t sh = take2 ? w2 : 0u;
-    const uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << sh;
-    c.hi = (uint32_t)(b >> 32);
-    c.lo = (uint32_t)b;
-    c.avail -= sh;
-    return n + (take2 ? 1u : 0u);
-}
+// The interior loops run while the parse is a margin short of every bound.  A step's reads past the bound
+// stay inside the block window (the last chunk's bound has the 256-bit slack behind it), so only the bits
+// a step takes must stay short of it: the table steps of both passes take <= 31 + 31 bits; the bounded
+// steps then finish the chunk.  (128, the window-read bound, before: sync 346 -> 311 us, mark 464 -> 442
+// us per c8 step with its former two-code step, A/B x 3 on one box, profiles/r05/c8_ab.)
+constexpr uint32_t kLeanMargin = 64;
+static_assert(31 + 31 < kLeanMargin && 31 * 8 < 256, "steps stay short of the bound");
 
 // Sync-pass step by table (round 5): a run of 1-bit codes as lean_step, a refill to >= 32 bits, then every
 // code that lies wholly in the next kEgLutBits bits at once, from a 4 KiB table of (codes, bits) per bit
 // pattern; no code complete in them (a code of more than kEgLutBits bits): one code by its leading zeros.
-// A step moves at most 31 + 31 bits (the lean loops' margin holds).  The sync pass needs only the count
-// and the exit, so the codes' individual boundaries are never formed.
+// A step moves at most 31 + 31 bits (kLeanMargin).  The sync pass needs only the count and the exit, so the
+// codes' individual boundaries are never formed.
+// Table width of the mark pass (12: 4 KiB, 5 blocks per CU beside its window and mark slots) and of the
+// sync pass (DCT3D_SYNC_LUT_BITS, default 12: 7 blocks per CU)
 constexpr int kEgLutBits = 12;
+#ifndef DCT3D_SYNC_LUT_BITS
+#define DCT3D_SYNC_LUT_BITS 12
+#endif
+constexpr int kSyncLutBits = DCT3D_SYNC_LUT_BITS;
+template <int B>
 struct EgLut {
-    uint8_t e[1 << kEgLutBits];  // codes complete within the pattern (low 4 bits), the bits they take (high 4)
+    uint8_t e[1 << B];  // codes complete within the pattern (low 4 bits), the bits they take (high 4)
 };
-constexpr EgLut make_eg_lut() {
-    EgLut t{};
-    for (int v = 0; v < (1 << kEgLutBits); v++) {
+template <int B>
+constexpr EgLut<B> make_eg_lut() {
+    EgLut<B> t{};
+    for (int v = 0; v < (1 << B); v++) {
         int p = 0, k = 0;
         for (;;) {
             int z = 0;
-            while (p + z < kEgLutBits && !((v >> (kEgLutBits - 1 - p - z)) & 1)) z++;
-            if (p + 2 * z + 1 > kEgLutBits) break;
+            while (p + z < B && !((v >> (B - 1 - p - z)) & 1)) z++;
+            if (p + 2 * z + 1 > B) break;
             p += 2 * z + 1;
             k++;
         }
@@ -556,10 +539,19 @@ constexpr EgLut make_eg_lut() {
     }
     return t;
 }
-__device__ constexpr EgLut kEgLut = make_eg_lut();
-static_assert(kEgLutBits <= 15, "counts and widths fit 4 bits");
+__device__ constexpr EgLut<kEgLutBits> kEgLut = make_eg_lut<kEgLutBits>();
+__device__ constexpr EgLut<kSyncLutBits> kSyncLut = make_eg_lut<kSyncLutBits>();
+// the block's copy of a table: 16-byte pieces, ordered by the staging's barrier
+template <int B>
+__device__ __forceinline__ void copy_lut(uint8_t* s_lut, const EgLut<B>& t) {
+    static_assert((1 << B) % (16 * kEgBlock) == 0, "whole 16-byte pieces per thread");
+#pragma unroll
+    for (int r = 0; r < (1 << B) / (16 * kEgBlock); r++)
+        *(uint4*)(s_lut + 16 * (threadIdx.x + r * kEgBlock)) = *(const uint4*)(t.e + 16 * (threadIdx.x + r * kEgBlock));
+}
+static_assert(kEgLutBits <= 15 && kSyncLutBits <= 15, "counts and widths fit 4 bits");
 
-template <class Rd>
+template <int B, class Rd>
 __device__ __forceinline__ uint32_t lean_step_lut(const Rd& s, const uint8_t* lut, Lean& c, bool& bad) {
     const uint32_t n1 = __builtin_clz(~c.hi | 1u);  // run of 1-bit codes, at most 31, never past avail
     uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
@@ -573,7 +565,7 @@ __device__ __forceinline__ uint32_t lean_step_lut(const Rd& s, const uint8_t* lu
     c.avail += need ? 32u : 0u;
     c.nx += need ? 1u : 0u;
     c.pre = s(c.nx);
-    const uint32_t e = lut[hi >> (32 - kEgLutBits)];
+    const uint32_t e = lut[hi >> (32 - B)];
     const uint32_t k = e & 15u;
     const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
     const bool one = k == 0u && zz < 16u;  // one code of 13 .. 31 bits
@@ -584,6 +576,43 @@ __device__ __forceinline__ uint32_t lean_step_lut(const Rd& s, const uint8_t* lu
     c.lo = (uint32_t)b;
     c.avail -= w;
     return n1 + (k ? k : (one ? 1u : 0u));
+}
+
+// The mark pass's table step: lean_step_lut that stops on the step's one possible mark.  d0: the values
+// before the next mark.  All k table codes are taken unless the step's values would pass 32 (two marks) or
+// the mark falls on the table's second .. k-th code, whose bit offsets the table does not give; then only
+// the first code (its width by clz).  The mark is then always the run's d0-th value or the first code: bit
+// p0 + d0 of the step.  A step moves at most 31 + 31 bits.  (Round 5: the two-code step before it -- a run
+// of <= 30, a code, a second code when buffered, 53 VALU with the mark -- against 46 VALU and 9 % / 25 %
+// fewer steps on ramp / uniform content: the pass 430 -> 356 us per c8 step although its 4 KiB table costs
+// a sixth block per CU, profiles/r05/mark_lut.)
+template <class Rd>
+__device__ __forceinline__ uint32_t lean_step_lut_mark(const Rd& s, const uint8_t* lut, Lean& c, bool& bad,
+                                                       uint32_t d0) {
+    const uint32_t n1 = __builtin_clz(~c.hi | 1u);
+    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
+    c.avail -= n1;
+    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
+    const bool need = c.avail < 32u;
+    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
+    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);
+    hi = need ? rh : hi;
+    lo = need ? rl : lo;
+    c.avail += need ? 32u : 0u;
+    c.nx += need ? 1u : 0u;
+    c.pre = s(c.nx);
+    const uint32_t e = lut[hi >> (32 - kEgLutBits)];
+    const uint32_t k = e & 15u;
+    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
+    const bool full = k != 0u && n1 + k <= 32u && d0 - n1 - 1u >= k - 1u;
+    const bool one = !full && zz < 16u;
+    bad = !full && zz >= 16u;
+    const uint32_t w = full ? e >> 4 : (one ? 2u * zz + 1u : 0u);
+    b = (((uint64_t)hi << 32) | lo) << w;
+    c.hi = (uint32_t)(b >> 32);
+    c.lo = (uint32_t)b;
+    c.avail -= w;
+    return n1 + (full ? k : (one ? 1u : 0u));
 }
 
 // The resolve walk of chunk t (pass 0 with resolve, below): e = the pass-0 exit of chunk t - 1 (~0u: it
@@ -644,9 +673,8 @@ __device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, u
 __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
     __shared__ uint32_t win[kSyncWinAlloc];
     __shared__ uint32_t s_exit[kEgBlock];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kEgLutBits];
-    static_assert((1 << kEgLutBits) == 16 * kEgBlock, "one 16-byte piece per thread");
-    *(uint4*)(s_lut + 16 * threadIdx.x) = *(const uint4*)(kEgLut.e + 16 * threadIdx.x);  // ordered by the staging's barrier
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kSyncLutBits];
+    copy_lut(s_lut, kSyncLut);
     const bool rs = iteration == 0 && resolve;
     const uint64_t b = blockIdx.x;
     const uint64_t first = rs ? (b ? b * (kEgBlock - 1) - 1 : 0) : b * kEgBlock;
@@ -668,14 +696,14 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
         // The chunk interior first, without bounds (kLeanMargin; by table: lean_step_lut), then the bounded
         // steps to the chunk end, then the checked steps; a long or invalid code leaves the lean loops
         // unconsumed.
-        const uint32_t fast_stop = stop > kSyncMargin ? stop - kSyncMargin : 0u;
+        const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
         // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
         // chunk end (a code running past the limit is invalid: the checked steps)
         const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
         Lean c = lean_from(r);
         bool bad = false;
         const WinRead rd{win};
-        while (!bad & (c.pos() < fast_stop)) n += lean_step_lut(rd, s_lut, c, bad);
+        while (!bad & (c.pos() < fast_stop)) n += lean_step_lut<kSyncLutBits>(rd, s_lut, c, bad);
         while (!bad & (c.pos() < bstop)) n += lean_step<true>(rd, c, bad, bstop - c.pos());
         lean_to(r, c);
         while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
@@ -715,6 +743,8 @@ constexpr uint32_t kMkSlot = 17;  // a chunk has at most 17 marks (<= 512 values
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     __shared__ uint32_t win[kSyncWinAlloc];
     __shared__ uint16_t s_mk[kEgBlock * kMkSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kEgLutBits];
+    copy_lut(s_lut, kEgLut);
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
     // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
     // (status[2] != 0) and the host reruns without speculation
@@ -749,40 +779,43 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
     const uint64_t gm0 = idx0 / kMarkVals;  // mark gm0 + k = mark of value idx0 + 32 k - ph
     uint32_t i = 0, code;
-    // Interior of the chunk: a step moves at most 30 + 31 + 31 bits and 32 values, so while the parse is
-    // kLeanMargin bits short of the chunk end and of the data limit, and 66 values short of the wanted count,
-    // none of the bounds below can bind -- a lean loop without them (a long or invalid code leaves it for
-    // the checked loop, which reads or reports it).
-    const uint32_t lim_end = min(end, limit);
-    const uint32_t fast_end = lim_end > kMarkMargin ? lim_end - kMarkMargin : 0u;
-    const uint32_t fast_rem = rem > 66u ? rem - 66u : 0u;
+    // Interior of the chunk: a step moves at most 31 + 31 bits and 32 values, so while the parse is
+    // kLeanMargin bits short of the chunk end and of the data limit none of the bounds below can bind -- a
+    // lean loop without them (a long or invalid code leaves it for the checked loop, which reads or reports
+    // it).  The lean loops run only in chunks that cannot hold the last wanted value (rem64 > 2 kChunkBits;
+    // the few others take the checked steps whole): there the value count never binds, and the loops test
+    // only the position (round 5: 53 -> 50 VALU per step with the running mark index and slot below).
+    const uint32_t lim_end = ends_here ? 0u : min(end, limit);
+    const uint32_t fast_end = lim_end > kLeanMargin ? lim_end - kLeanMargin : 0u;
     {
         Lean c = lean_from(r);
         bool bad = false;
         const WinRead rd{win};
-        // a step takes nv <= 32 values, value i + d at bit p0 + d: at most one mark, value i + d0
-        auto mark = [&](uint32_t p0, uint32_t nv) {
-            const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
-            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(p0 + d0 - sp);  // no branch
+        // the next mark: chunk-relative value index nm (value idx0 + nm), its slot mp; a step takes nv <= 32
+        // values, so at most one mark, value d0 = nm - i of the step
+        uint32_t nm = (0u - ph) & (kMarkVals - 1);
+        uint16_t* mp = myk + (ph + nm) / kMarkVals;
+        const uint32_t s0 = 0u - sp;  // (bit positions leave relative to the chunk's true start)
+        auto mark = [&](uint32_t at, uint32_t nv, uint32_t d0) {
+            const bool hit = d0 < nv;
+            *(hit ? mp : dummy) = (uint16_t)(at + s0);  // no branch
+            nm += hit ? kMarkVals : 0u;
+            mp += hit ? 1 : 0;
             i += nv;
         };
-        // two-code steps (a run of <= 30, a code, a second code when buffered: nv <= 32): value i + d at bit
-        // p0 + d for d <= n1 (the run, then the first code), the second code at p0 + n1 + w
-        while (!bad & (c.pos() < fast_end) & (i < fast_rem)) {
+        // table steps that stop on the mark (nv <= 32): the mark is value d0 of the step, at bit p0 + d0
+        while (!bad & (c.pos() < fast_end)) {
             const uint32_t p0 = c.pos();
-            uint32_t n1, w;
-            const uint32_t nv = lean_step2<30u>(rd, c, bad, &n1, &w);
-            const uint32_t d0 = (0u - (ph + i)) & (kMarkVals - 1);
-            const uint32_t at = p0 + d0 + (d0 > n1 ? w - 1u : 0u);
-            *(d0 < nv ? myk + (ph + i + d0) / kMarkVals : dummy) = (uint16_t)(at - sp);  // no branch
-            i += nv;
+            const uint32_t d0 = nm - i;
+            mark(p0 + d0, lean_step_lut_mark(rd, s_lut, c, bad, d0), d0);
         }
         // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
         // end take the checked steps)
-        const uint32_t bend = limit >= end + 64u ? end : 0u;
-        while (!bad & (c.pos() < bend) & (i < fast_rem)) {
+        const uint32_t bend = limit >= end + 64u && !ends_here ? end : 0u;
+        while (!bad & (c.pos() < bend)) {
             const uint32_t p0 = c.pos();
-            mark(p0, lean_step<true>(rd, c, bad, bend - p0));
+            const uint32_t d0 = nm - i;
+            mark(p0 + d0, lean_step<true>(rd, c, bad, bend - p0), d0);
         }
         lean_to(r, c);
     }
