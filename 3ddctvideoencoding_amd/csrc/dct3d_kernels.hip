@@ -192,7 +192,11 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     const uint32_t wid = blockIdx.x * kWavesPerBlock + wave;  // segment index
     const uint32_t cube0 = wid * kCubesPerWave;
     uint2 raw[D];
-    load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);  // in flight first
+    // the rows in flight first, issued at the top priority (as encode16_kernel's: under oldest-first issue
+    // they queue behind the computing waves' VALU work; c7 -0.4 %, profiles/r05/c7_ab/7_prio)
+    __builtin_amdgcn_s_setprio(3);
+    load_rows<D>(P, cube0 + (lane >> 3), cube0 + (lane >> 3) < P.n_cubes, lane & 7, raw);
+    __builtin_amdgcn_s_setprio(0);
     {  // both loads in flight before the LDS writes (a strided loop waited one round trip per pass)
         static_assert(CS % kBlock == 0, "whole passes");
         uint16_t t[CS / kBlock];
@@ -618,11 +622,18 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         }
         uint64_t gb_n = 0, last_n = 0;
         uint32_t myl_n = 0;
+        // the look-ahead loads at the top priority (as the first group's): issued ahead of the other waves'
+        // parse and transform work, not behind it (consumer 2,520 -> 2,454 us per c8 step,
+        // profiles/r05/consumer/prio)
+        __builtin_amdgcn_s_setprio(3);
         if (i + 1 < NG) load_marks(lane, cube_of(i + 1), gb_n, myl_n, last_n);  // in flight during the parse
+        __builtin_amdgcn_s_setprio(0);
         wave_lds_sync();
         uint32_t v[32];  // codes: decode_tile<CODES> converts them in its dequantisation
         parse_codes<32>(E, win, nwin, w0, fits, long_codes, w0 * 32 + rel, v);
+        __builtin_amdgcn_s_setprio(3);
         if (i + 1 < NG) open_window(lane, gb_n, myl_n, last_n, w0, rel, span, pw);  // in flight during the transform
+        __builtin_amdgcn_s_setprio(0);
         wave_lds_sync();
         {  // each value to its diagonal position in the staging: 8 offsets per 16-byte table read
             const uint32_t c = lane / PARTS, part = lane % PARTS;
