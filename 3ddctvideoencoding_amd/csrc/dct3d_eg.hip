@@ -789,10 +789,14 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const LdsBits L = stage_block_window(P, win);
     const uint64_t t = first + threadIdx.x;
     if (t >= P.n_chunks) return;
+    // the chunk's first value index and true start: both loads in flight together, at the top issue
+    // priority (one round trip, not two behind the other blocks' parse work)
+    __builtin_amdgcn_s_setprio(3);
     const uint64_t idx0 = P.off[t];
-    if (idx0 >= P.n_values) return;
     // the converged exits are in exit_in (the host swaps the buffers after every pass)
     const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
+    __builtin_amdgcn_s_setprio(0);
+    if (idx0 >= P.n_values) return;
     if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
     const uint64_t base = L.w0 * 32;
     const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
