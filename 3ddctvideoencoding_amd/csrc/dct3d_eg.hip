@@ -769,8 +769,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
 // mark is stored branch-free: steps without a mark store to the thread's dummy, 2 bytes behind the
 // window (round 4: an 18th slot entry; an exec-masked store instead compiled to a branch and 13 more VALU
 // per step).
-// Marks leave as the low 32 bits of their bit position (round 5; 64-bit before: 0.52 GB written and read
-// back per c8 step), the whole position of every 64th (a consumer group's first) in mark_base.
+// Marks leave as the low 16 bits of their bit position (round 5; 64-bit before: 0.52 GB written and read
+// back per c8 step, then 32-bit: 0.27 GB), the whole position of every 64th (a consumer group's first) in
+// mark_base (mark_offset).
 constexpr uint32_t kMkSlot = 17;  // a chunk has at most 17 marks (<= 512 values)
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     __shared__ uint32_t win[kSyncWinAlloc];
@@ -889,10 +890,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     }
     // the chunk's marks k = (ph ? 1 : 0) .. (ph + i - 1) / 32, back to back
     const uint64_t b0 = base + sp;
-    uint32_t* const mk = P.mark + gm0;
+    uint16_t* const mk = P.mark + gm0;
     for (uint32_t k = ph ? 1u : 0u; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) {
         const uint64_t m = b0 + myk[k];
-        mk[k] = (uint32_t)m;
+        mk[k] = (uint16_t)m;
         if (((gm0 + k) & (kMarkGroup - 1)) == 0) P.mark_base[(gm0 + k) / kMarkGroup] = m;
     }
 }
@@ -913,9 +914,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     const bool lv = m0 + lane < n_marks;
     static_assert(kMarkGroup == 64, "a wave = one mark group");
     const uint64_t gb = P.mark_base[m0 / kMarkGroup];  // wave-uniform
-    const uint64_t my = lv ? mark_at(P, m0 + lane, gb) : 0;
     const uint64_t first = gb;
     const uint64_t last = m0 + 64 < n_marks ? P.mark_base[m0 / kMarkGroup + 1] : P.status[1];  // wave-uniform
+    const uint32_t off = mark_offset(lv ? P.mark[m0 + lane] : 0u, (uint16_t)gb);
+    const uint64_t my = lv ? gb + off : 0;
     const uint64_t w0 = first >> 5;
     const uint64_t span = (last >> 5) + 5 - w0;  // + 5 words of slack: parse_win
     const bool fits = span <= kEmitWinWords - 1;  // wave-uniform
@@ -938,7 +940,8 @@ __global__ __launch_bounds__(kEgBlock) void eg_emit_kernel(EgDecParams P) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t v[kMarkVals];
-    parse_codes<kMarkVals>(P, win, nwin, w0, fits, P.status[3] != 0, my, v);
+    parse_codes<kMarkVals>(P, win, nwin, w0, fits, P.status[3] != 0,
+                           my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u, v);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -271,14 +271,15 @@ __device__ __forceinline__ void parse_win(const uint32_t* win, uint32_t p, uint3
 // (then unused) window region, lane-private rows of N words (64 N words: every caller's region holds
 // them), so that cd is written at constant indices only (a runtime index into cd would make a caller's
 // loop carry all of cd: decode_eg_kernel).
+// p: the lane's first bit relative to bit 32 w0 (the window's first).
 template <int N>
 __device__ __forceinline__ void parse_codes(const EgDecParams& P, uint32_t* win, uint32_t nwin, uint64_t w0,
-                                            bool fits, bool long_codes, uint64_t my, uint32_t (&cd)[N]) {
+                                            bool fits, bool long_codes, uint32_t p, uint32_t (&cd)[N]) {
     if (fits) {
-        const uint32_t p = my > w0 * 32 ? (uint32_t)min(my - w0 * 32, (uint64_t)0xFFFFFFFFu) : 0u;
         if (long_codes) parse_win<N, true>(win, p, cd);
         else parse_win<N, false>(win, p, cd);
     } else {
+        const uint64_t my = w0 * 32 + p;
         uint32_t* row = (win - 1) + (threadIdx.x & 63) * N;  // from the region's first word
         BitReader<GlobalBits> r{GlobalBits{P.words, P.n_words}, 0, 0, 0, 0, 0};
         r.seek(my);

@@ -91,9 +91,12 @@ struct EgParams {
 
 // Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)
 constexpr uint64_t kEgChunkBits = 512;  // bits per parse chunk (one thread each)
-// Marks (the bit position of every 32nd value) are stored as 32-bit low halves; the marks of a group of
-// kMarkGroup (a consumer wave's 2,048 values) lie within 2^32 bits of the group's first (a value's code
-// has < 64 bits), whose whole position is kept in mark_base: mark_at() rebuilds a 64-bit position.
+// Marks (the bit position of every 32nd value) are stored as their low 16 bits; the whole position of a
+// group's first (kMarkGroup marks: a consumer wave's 2,048 values) is kept in mark_base.  Consecutive
+// marks lie < 2^16 bits apart (32 codes of < 64 bits), so a mark's offset from its group's first is the
+// sum of the 16-bit differences up to it: a wave holding the group's 64 marks counts the wraps
+// (mark_offset), a single lane adds the differences (mark_serial).  (Round 5: 32-bit low halves before,
+// 0.27 GB written by the mark pass and read back by the consumer per c8 step.)
 constexpr uint64_t kMarkGroup = 64;
 struct EgDecParams {
     const uint32_t* words;     // stream, memory byte order
@@ -108,7 +111,7 @@ struct EgDecParams {
     uint32_t* count;           // codewords per chunk
     uint64_t* off;             // value index of each chunk's first codeword (scan)
     uint64_t* status;          // [0] changed / first invalid chunk, [1] end bit, [2] flags 1 corrupt, [3] values
-    uint32_t* mark;            // [n_values / 32] bit position of every 32nd value, low 32 bits
+    uint16_t* mark;            // [n_values / 32] bit position of every 32nd value, low 16 bits
     uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output
 };
@@ -129,9 +132,27 @@ struct EgFusedParams {
     uint32_t* seg_bits;        // [n_seg] bits per segment (the scan's input)
 };
 
-// the whole bit position of mark m (its group's base: mark_base[m / kMarkGroup], read once per group)
-__device__ __forceinline__ uint64_t mark_at(const EgDecParams& P, uint64_t m, uint64_t group_base) {
-    return group_base + (uint32_t)(P.mark[m] - (uint32_t)group_base);
+// Lane l of a wave holding a group's marks in order (lane 0: the group's first, base_low its low 16 bits;
+// lanes past the last mark: any value) -> the offset of its mark from the group's first: the 16-bit
+// difference r_l plus 2^16 per wrap at or below l (a wrap: r_l < r_{l-1}).  All 64 lanes take part.
+__device__ __forceinline__ uint32_t mark_offset(uint32_t low, uint32_t base_low) {
+    const uint32_t r = (low - base_low) & 0xFFFFu;
+    const uint32_t prev = __shfl_up(r, 1);  // lane 0: its own (0)
+    const bool wrap = r < prev;
+    const uint64_t wraps = __ballot(wrap);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(wraps >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wraps, 0u));
+    return r + ((below + (uint32_t)wrap) << 16);
+}
+// the whole bit position of mark m, one lane alone (the exact replay): the differences from its group's first
+__device__ __forceinline__ uint64_t mark_serial(const uint16_t* mark, const uint64_t* mark_base, uint64_t m) {
+    const uint64_t g0 = m & ~(kMarkGroup - 1), gb = mark_base[m / kMarkGroup];
+    uint32_t off = 0, prev = (uint16_t)gb;
+    for (uint64_t k = g0 + 1; k <= m; k++) {
+        const uint32_t c = mark[k];
+        off += (c - prev) & 0xFFFFu;
+        prev = c;
+    }
+    return gb + off;
 }
 
 int launch_decode(int D, const DecodeParams& P, hipStream_t st);

@@ -479,15 +479,14 @@ template <int D>
 struct ReloadStream {
     const uint32_t* words;
     uint64_t n_words;
-    const uint32_t* mark;
+    const uint16_t* mark;
     const uint64_t* mark_base;
     const uint16_t* diag;  // the block's LDS copy
     __device__ __forceinline__ void operator()(uint32_t g, double* cf, int lane) const {
         constexpr int PARTS = 64 * D / 32;
         if (lane < PARTS) {
             BitReader<GlobalBits> r{GlobalBits{words, n_words}, 0, 0, 0, 0};
-            const uint64_t m = (uint64_t)g * PARTS + lane, gb = mark_base[m / kMarkGroup];
-            r.seek(gb + (uint32_t)(mark[m] - (uint32_t)gb));  // mark_at
+            r.seek(mark_serial(mark, mark_base, (uint64_t)g * PARTS + lane));
             for (int i = 0; i < 32; i++) {
                 uint32_t code = 1u;
                 (void)r.get(code);
@@ -548,15 +547,15 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     const uint64_t n_marks = E.n_values / 32;
     const uint32_t row0 = xcd_tile() * NG;  // the block's first round of 4 groups
     auto cube_of = [&](int i) { return P.cube_base + ((row0 + (uint32_t)i) * kWavesPerBlock + wave) * CPW; };
-    // the group's marks as loaded: its first (a whole position), the lane's low 32 bits (value 32 * (m0 +
-    // lane); a lane past the last mark: the first's) and the end of its bit range (all lanes alike).  They
+    // the group's marks as loaded: its first (a whole position), the lane's low 16 bits (value 32 * (m0 +
+    // lane); a lane past the last mark: ~0u) and the end of its bit range (all lanes alike).  They
     // are combined in open_window, after the parse they are loaded across (combined here, the wait for them
     // sat before the parse)
     static_assert(kMarkGroup == 64, "a group = one mark group");
     auto load_marks = [&](int lane, uint32_t cube0, uint64_t& gb, uint32_t& myl, uint64_t& last) {
         const uint64_t m0 = (uint64_t)cube0 * CS / 32;
         gb = E.mark_base[m0 / kMarkGroup];
-        myl = m0 + lane < n_marks ? E.mark[m0 + lane] : 0u;
+        myl = m0 + lane < n_marks ? (uint32_t)E.mark[m0 + lane] : ~0u;
         last = m0 + 64 < n_marks ? E.mark_base[m0 / kMarkGroup + 1] : E.status[1];
     };
     // window of a group: first word w0 (the first mark's), the lane's mark relative to bit 32 w0, the
@@ -564,11 +563,10 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     auto open_window = [&](int lane, uint64_t gb, uint32_t myl, uint64_t last, uint64_t& w0, uint32_t& rel,
                            uint64_t& span, uint32_t (&t)[NWP]) {
         w0 = uniform_u64(gb >> 5);  // the group's first mark
-        // mark_at, relative to bit 32 w0: < 2^17 for a real mark (a group spans < 2^17 bits); a lane past
-        // the last mark (myl = 0, the unused cubes of a partial last group: ~2^32) parses from the window's
-        // first bit, inside the window
-        const uint64_t d = gb + (uint32_t)(myl - (uint32_t)gb) - w0 * 32;
-        rel = d < (1ull << 20) ? (uint32_t)d : 0u;
+        // relative to bit 32 w0: the mark's offset from the group's first, + gb % 32; a lane past the last
+        // mark (the unused cubes of a partial last group) parses from the window's first bit, inside the window
+        const uint32_t off = mark_offset(myl, (uint16_t)gb);
+        rel = myl <= 0xFFFFu ? (uint32_t)(gb & 31) + off : 0u;
         const uint64_t lw = uniform_u64(last);
         span = (lw >> 5) + 5 - w0;
         // word w0 + j from a scalar base, j clamped into the stream in 32 bits (a look-ahead past the last
@@ -636,7 +634,7 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
         __builtin_amdgcn_s_setprio(2);
         wave_lds_sync();
         uint32_t v[32];  // codes: decode_tile<CODES> converts them in its dequantisation
-        parse_codes<32>(E, win, nwin, w0, fits, long_codes, w0 * 32 + rel, v);
+        parse_codes<32>(E, win, nwin, w0, fits, long_codes, rel, v);
         __builtin_amdgcn_s_setprio(3);
         if (i + 1 < NG) open_window(lane, gb_n, myl_n, last_n, w0, rel, span, pw);  // in flight during the transform
         __builtin_amdgcn_s_setprio(2);

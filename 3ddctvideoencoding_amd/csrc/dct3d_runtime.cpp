@@ -980,7 +980,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
     const uint64_t n_marks = n_cubes * (uint64_t)c->plan.cs / 32;
     const uint64_t n_mark_groups = n_marks / kMarkGroup + 1;
-    if (!rc) rc = c->d_egd_mark.grow(n_mark_groups * sizeof(uint64_t) + (n_marks + 1) * sizeof(uint32_t));
+    if (!rc) rc = c->d_egd_mark.grow(n_mark_groups * sizeof(uint64_t) + (n_marks + 1) * sizeof(uint16_t));
     if (rc) return rc;
     D.words = (const uint32_t*)d_bytes;
     D.n_words = (nbytes + 3) / 4;
@@ -995,7 +995,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.off = (uint64_t*)c->d_eg_off.p;
     D.status = (uint64_t*)c->d_egd_status.p;
     D.mark_base = (uint64_t*)c->d_egd_mark.p;
-    D.mark = (uint32_t*)(D.mark_base + n_mark_groups);
+    D.mark = (uint16_t*)(D.mark_base + n_mark_groups);
     D.q = nullptr;
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts and, resolving,
     // usually proves every chunk in sync by itself; otherwise confirming passes follow); at most
