@@ -292,15 +292,18 @@ def test_fused_decode_sparse_long_codes(pkg, oracle, plan8, plan4, gpu_ctx8, gpu
 
 
 @pytest.mark.parametrize("depth", [8, 4])
-def test_fused_decode_long_codes_everywhere_in_window(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth):
-    """Every value a 33-bit code (|q| in [2^15, 2^16)): a consumer group's 2,048 values span ~67.6 k bits,
-    wider than 2^16 and still inside the consumer's LDS window -- the flagged (checking) parse steps in the
-    window, marks far apart, and the exact replay of every cube (out-of-range coefficients), which re-reads
-    its values from the stream at the marks."""
+@pytest.mark.parametrize("lo", [15, 19])
+def test_fused_decode_long_codes_everywhere_in_window(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, lo):
+    """Every value a long code.  lo = 15: 33-bit codes (|q| in [2^15, 2^16)), a consumer group's 2,048
+    values span ~67.6 k bits, wider than 2^16 (the 16-bit marks wrap inside the group: mark_offset) and
+    still inside the consumer's LDS window -- the flagged (checking) parse steps in the window, marks far
+    apart, and the exact replay of every cube (out-of-range coefficients), which re-reads its values from
+    the stream at the marks (mark_serial).  lo = 19: 39..41-bit codes, ~82 k bits per group, past the
+    window: the parse from global memory at the rebuilt marks."""
     ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
-    rng = np.random.default_rng(31 + depth)
+    rng = np.random.default_rng(31 + depth + lo)
     n = ctx.n_cubes(64, 48, 2)
-    q = rng.integers(2**15, 2**16, size=(n, depth, 8, 8)) * rng.choice([-1, 1], size=(n, depth, 8, 8))
+    q = rng.integers(2**lo, 2**(lo + 1), size=(n, depth, 8, 8)) * rng.choice([-1, 1], size=(n, depth, 8, 8))
     q = q.astype(np.int32)
     data, nbits = _expected(oracle, pkg, q, depth)
     got, eb = _decode_fused(ctx, data, 64, 48, 2)
