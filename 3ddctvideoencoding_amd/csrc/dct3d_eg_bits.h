@@ -225,7 +225,7 @@ __device__ __forceinline__ void parse_step(const uint32_t* win, int32_t& n, uint
 #pragma unroll
     for (int e = 0; e < C; e++) {
         nw[e] = eg_negwidth(__builtin_clz(b[0]));
-        code[e] = b[0] >> (uint32_t)nw[e];
+        code[e] = b[0] >> ((uint32_t)nw[e] & 31u);  // the low 5 bits: 32 - width (v_lshrrev reads no others)
         if constexpr (CHECK) mn = min(mn, b[0]);
 #pragma unroll
         for (int j = 0; j + 1 < C - e; j++) b[j] = __builtin_amdgcn_alignbit(b[j], b[j + 1], (uint32_t)nw[e]);

@@ -110,7 +110,10 @@ struct EgDecParams {
     uint64_t* exit_out;
     uint32_t* count;           // codewords per chunk
     uint64_t* off;             // value index of each chunk's first codeword (scan)
-    uint64_t* status;          // [0] changed / first invalid chunk, [1] end bit, [2] flags 1 corrupt, [3] values
+    // [0] changed / first invalid chunk, [1] end bit, [2] flags (1 corrupt, 2 short, 4 rerun), [3] a code of
+    // 33+ bits seen (mark pass; the consumers then parse with CHECK); zeroed with the other words by
+    // eg_decode_front's memset before every pass
+    uint64_t* status;
     uint16_t* mark;            // [n_values / 32] bit position of every 32nd value, low 16 bits
     uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output

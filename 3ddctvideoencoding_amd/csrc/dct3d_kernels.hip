@@ -554,7 +554,9 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     static_assert(kMarkGroup == 64, "a group = one mark group");
     auto load_marks = [&](int lane, uint32_t cube0, uint64_t& gb, uint32_t& myl, uint64_t& last) {
         const uint64_t m0 = (uint64_t)cube0 * CS / 32;
-        gb = E.mark_base[m0 / kMarkGroup];
+        // a wave past the last group (or the look-ahead of the group after it) reads no mark_base entry:
+        // it holds n_marks / kMarkGroup + 1 of them
+        gb = m0 < n_marks ? E.mark_base[m0 / kMarkGroup] : 0u;
         myl = m0 + lane < n_marks ? (uint32_t)E.mark[m0 + lane] : ~0u;
         last = m0 + 64 < n_marks ? E.mark_base[m0 / kMarkGroup + 1] : E.status[1];
     };

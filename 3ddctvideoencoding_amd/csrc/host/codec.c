@@ -23,10 +23,29 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "codec.h"
 #include "codec_entropy.h"
 #include "dct3d.h"
+
+/* DCT3D_CODEC_TIMING=1: encode_ex / decode_ex print one JSON line of per-stage wall seconds to stderr
+ * (tools/codec_e2e.py): which stage bounds the reference-identical .bin end to end */
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+static int timing_on(void) {
+    const char *e = getenv("DCT3D_CODEC_TIMING");
+    return e && e[0] == '1';
+}
+#define STAGE(acc, stmt)              \
+    do {                              \
+        const double t_0_ = now_s();  \
+        stmt;                         \
+        (acc) += now_s() - t_0_;      \
+    } while (0)
 
 static int default_batch(void) {
     const char *e = getenv("DCT3D_CODEC_BATCH");
@@ -54,7 +73,10 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
         return 1;
     }
     dct3d_ctx *ctx = NULL;
+    const double t_start = now_s();
+    double t_read = 0, t_dev = 0, t_fetch = 0, t_ent = 0;
     int rc = dct3d_ctx_create(platformIndex > 0 ? platformIndex - 1 : 0, 8, 8, depth, &ctx);
+    const double t_ctx = now_s() - t_start;
     if (rc) {
         printf("Error creating the device context: %s\n", dct3d_strerror(rc));
         fclose(in);
@@ -89,16 +111,17 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
         const int nb = (n_stacks - s0) < batch ? (n_stacks - s0) : batch;
         size_t got = 0, r;
         const size_t want = stack_px * nb;
-        while (got < want && (r = fread(raster + got, 1, want - got, in)) > 0) got += r;
+        STAGE(t_read, while (got < want && (r = fread(raster + got, 1, want - got, in)) > 0) got += r);
         if (got < want) memset(raster + got, 0, want - got);
         const int last = s0 + nb == n_stacks;
         if (host_eg) {  /* quantised ints over PCIe, Exp-Golomb on the host (the reference's split) */
-            rc = dct3d_encode_stacks(ctx, raster, width, height, nb, q, NULL);
+            STAGE(t_dev, rc = dct3d_encode_stacks(ctx, raster, width, height, nb, q, NULL));
             if (rc) {
                 printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
                 status = 1;
                 break;
             }
+            const double t_e0 = now_s();
             for (int s = 0; s < nb; s++) {
                 if (dct3d_entropy_enc_push(ent, q + stack_px * s, s0 + s == n_stacks - 1)) {
                     printf("Error in the entropy coder\n");
@@ -106,12 +129,13 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
                     break;
                 }
             }
+            t_ent += now_s() - t_e0;
         } else {  /* DCT + quantisation + diagonal order + Exp-Golomb on the device; the stream over PCIe */
             uint8_t cb;
             int cbits;
             uint64_t tb = 0;
             dct3d_entropy_enc_carry(ent, &cb, &cbits);
-            rc = dct3d_encode_eg(ctx, raster, width, height, nb, cb, cbits, &tb);
+            STAGE(t_dev, rc = dct3d_encode_eg(ctx, raster, width, height, nb, cb, cbits, &tb));
             const size_t nbytes = (size_t)((tb + 7) / 8);
             if (!rc && nbytes > eg_cap) {
                 free(eg);
@@ -119,13 +143,15 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
                 eg = (unsigned char *)malloc(eg_cap);
                 if (!eg) rc = DCT3D_ENOMEM;
             }
-            if (!rc) rc = dct3d_eg_fetch(ctx, eg, nbytes);
+            if (!rc) STAGE(t_fetch, rc = dct3d_eg_fetch(ctx, eg, nbytes));
             if (rc) {
                 printf("Error running the 3D DCT: %s\n", dct3d_strerror(rc));
                 status = 1;
                 break;
             }
-            if (dct3d_entropy_enc_push_stream(ent, eg, tb, last)) {
+            int perr;
+            STAGE(t_ent, perr = dct3d_entropy_enc_push_stream(ent, eg, tb, last));
+            if (perr) {
                 printf("Error in the entropy coder\n");
                 status = 1;
                 break;
@@ -133,13 +159,19 @@ int encode_ex(const char *inName, const char *outName, int width, int height, in
         }
         for (int s = 0; !status && s < nb; s++) printf("Frames processed: %d\n", (s0 + s + 1) * depth);
     }
-    dct3d_entropy_enc_destroy(ent);
+    STAGE(t_ent, dct3d_entropy_enc_destroy(ent));  /* the last deflate output and its write */
     free(raster);
     free(q);
     free(eg);
     dct3d_ctx_destroy(ctx);
     fclose(in);
     if (fflush(out) || fclose(out)) status = 1;
+    if (timing_on())
+        fprintf(stderr,
+                "{\"stage_s\": {\"ctx_create\": %.6f, \"read\": %.6f, \"device\": %.6f, \"eg_fetch\": %.6f, "
+                "\"%s\": %.6f}, \"total_s\": %.6f, \"host_eg\": %d, \"deflate_threads\": %d}\n",
+                t_ctx, t_read, t_dev, t_fetch, host_eg ? "eg_deflate_write" : "deflate_write", t_ent, now_s() - t_start,
+                host_eg, deflate_threads);
     if (!status) printf("Encoding process completed\n");
     return status;
 }
@@ -163,7 +195,10 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
         return 1;
     }
     dct3d_ctx *ctx = NULL;
+    const double t_start = now_s();
+    double t_inf = 0, t_dev = 0, t_write = 0;
     int rc = dct3d_ctx_create(platformIndex > 0 ? platformIndex - 1 : 0, 8, 8, depth, &ctx);
+    const double t_ctx = now_s() - t_start;
     if (rc) {
         printf("Error creating the device context: %s\n", dct3d_strerror(rc));
         fclose(in);
@@ -188,14 +223,16 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
     for (int s0 = 0; !status && s0 < n_stacks; s0 += batch) {
         const int nb = (n_stacks - s0) < batch ? (n_stacks - s0) : batch;
         if (host_eg) {
+            const double t_i0 = now_s();
             for (int s = 0; s < nb; s++)
                 if (dct3d_entropy_dec_pull(ent, q + stack_px * s)) {
                     printf("Truncated or corrupt input stream\n");
                     status = 1;
                     break;
                 }
+            t_inf += now_s() - t_i0;
             if (status) break;
-            rc = dct3d_decode_stacks(ctx, q, width, height, nb, raster);
+            STAGE(t_dev, rc = dct3d_decode_stacks(ctx, q, width, height, nb, raster));
         } else {
             const double values = (double)stack_px * nb;
             size_t need = (size_t)(values * bits_per_value / 8 * 1.25) + 65536;
@@ -204,11 +241,13 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
                 size_t len;
                 int bit;
                 uint64_t eb = 0;
-                if (dct3d_entropy_dec_window(ent, need, &p, &len, &bit)) {
+                int werr;
+                STAGE(t_inf, werr = dct3d_entropy_dec_window(ent, need, &p, &len, &bit));
+                if (werr) {
                     rc = DCT3D_EINVAL;
                     break;
                 }
-                rc = dct3d_decode_eg(ctx, p, len, bit, width, height, nb, raster, &eb);
+                STAGE(t_dev, rc = dct3d_decode_eg(ctx, p, len, bit, width, height, nb, raster, &eb));
                 if (rc == DCT3D_ENODATA && !dct3d_entropy_dec_eof(ent) && len >= need) {
                     need *= 2;  /* the batch needs more of the stream than estimated */
                     continue;
@@ -230,7 +269,9 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
             status = 1;
             break;
         }
-        if (fwrite(raster, 1, stack_px * nb, out) != stack_px * nb) {
+        size_t wrote;
+        STAGE(t_write, wrote = fwrite(raster, 1, stack_px * nb, out));
+        if (wrote != stack_px * nb) {
             printf("Error writing the output file\n");
             status = 1;
             break;
@@ -242,7 +283,12 @@ int decode_ex(const char *inName, const char *outName, int width, int height, in
     free(q);
     dct3d_ctx_destroy(ctx);
     fclose(in);
-    if (fflush(out) || fclose(out)) status = 1;
+    STAGE(t_write, if (fflush(out) || fclose(out)) status = 1);
+    if (timing_on())
+        fprintf(stderr,
+                "{\"stage_s\": {\"ctx_create\": %.6f, \"%s\": %.6f, \"device\": %.6f, \"write\": %.6f}, "
+                "\"total_s\": %.6f, \"host_eg\": %d}\n",
+                t_ctx, host_eg ? "read_inflate_eg" : "read_inflate", t_inf, t_dev, t_write, now_s() - t_start, host_eg);
     if (!status) printf("Decoding process completed\n");
     return status;
 }

@@ -373,3 +373,20 @@ def test_fused_decode_groups_per_wave(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_c
         got, eb = _decode_fused(ctx, data, 64, 48, 2)
     assert eb == nbits
     assert np.array_equal(got, plan.decode_q(q, 64, 48, 2 * depth))
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("w,h", [(8, 8), (16, 8), (24, 8), (16, 16)])
+def test_fused_decode_tiny_frames(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, w, h):
+    """1 to 4 cubes: one partial consumer group, waves (and look-ahead groups) past the last mark group,
+    whose mark_base entry does not exist and must not be read; both consumers."""
+    ctx, plan = (gpu_ctx8, plan8) if depth == 8 else (gpu_ctx4, plan4)
+    fr = pkg.synthetic.frames(w, h, depth, kind="uniform", frame0=w * h + depth)
+    q = plan.encode_q(fr)
+    data, nbits = _expected(oracle, pkg, q, depth)
+    got, eb = _decode_fused(ctx, data, w, h, 1)
+    assert eb == nbits
+    assert np.array_equal(got, plan.decode_q(q, w, h, depth))
+    n = ctx.n_cubes(w, h, 1)
+    qd, eb2 = _eg_decode_q(ctx, data, n)
+    assert eb2 == nbits and np.array_equal(qd, q.reshape(n, depth, 8, 8))
