@@ -32,6 +32,7 @@ DCT3D_OK, DCT3D_EINVAL, DCT3D_EDEVICE, DCT3D_ENOMEM, DCT3D_EKERNEL, DCT3D_ENOSPC
 DCT3D_OPT_DEC_MARGIN, DCT3D_OPT_ENC_NO_RECHECK, DCT3D_OPT_EG_TWO_STEP, DCT3D_OPT_EG_NO_RESOLVE = 2, 3, 5, 6
 DCT3D_OPT_EG_FORCE_RETRY = 8
 DCT3D_OPT_EG_DEC_GROUPS = 9
+DCT3D_OPT_EG_FUSED_FRONT = 10
 
 # Every symbol include/dct3d.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = (
@@ -46,7 +47,7 @@ ABI_SYMBOLS = (
 )
 # Every symbol include/dct3d_diag.h declares (libdct3d_diag.so; none of them is in libdct3d.so).
 DIAG_SYMBOLS = ("dct3d_fill_synthetic_dev", "dct3d_bandwidth_probe_dev", "dct3d_encode_memonly_dev",
-                "dct3d_encode_diag_dev", "dct3d_encode_trace_dev", "dct3d_decode_diag_dev")
+                "dct3d_encode_diag_dev", "dct3d_encode_trace_dev", "dct3d_encode_strip_dev", "dct3d_decode_diag_dev")
 
 
 class Dct3dError(RuntimeError):
@@ -137,6 +138,7 @@ def diag_lib() -> C.CDLL:
         D.dct3d_bandwidth_probe_dev.argtypes = [vp, vp, vp, sz, i32]
         D.dct3d_encode_memonly_dev.argtypes = [vp, vp, i32, i32, i32, vp]
         D.dct3d_encode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
+        D.dct3d_encode_strip_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32, i32]
         D.dct3d_encode_trace_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32, vp]
         D.dct3d_decode_diag_dev.argtypes = [vp, vp, i32, i32, i32, vp, i32]
         _diag = D
@@ -317,6 +319,11 @@ class Context:
         """Diagnostic: the encode's memory traffic without its compute (d_q is NOT a DCT)."""
         _check(diag_lib().dct3d_encode_memonly_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q)),
                "dct3d_encode_memonly_dev")
+
+    def encode_strip_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q, mode: int, strip_w: int) -> None:
+        """diagnostic traversal sweep (dct3d_encode_strip_dev): mode 1 memory only, mode 0 the full encode"""
+        _check(diag_lib().dct3d_encode_strip_dev(self._h, _tptr(d_frames), width, height, n_stacks, _tptr(d_q), mode,
+                                                 strip_w), "dct3d_encode_strip_dev")
 
     def encode_diag_dev(self, d_frames, width: int, height: int, n_stacks: int, d_q, mode: int) -> None:
         """Diagnostic: the encode's memory part (mode 1) or, 8x8x8, its compute part (mode 2) alone."""

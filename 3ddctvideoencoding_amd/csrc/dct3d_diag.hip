@@ -334,14 +334,27 @@ int dct3d_encode_diag_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, i
     return dct3d_encode_trace_dev(c, d_raster, w, h, n_stacks, d_q, mode, nullptr);
 }
 
+static int encode_diag(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode,
+                       uint64_t* d_trace, int strip_w);
 int dct3d_encode_trace_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode,
                            uint64_t* d_trace) {
+    return encode_diag(c, d_raster, w, h, n_stacks, d_q, mode, d_trace, 0);
+}
+
+int dct3d_encode_strip_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode,
+                           int strip_w) {
+    if ((mode != 0 && mode != 1) || strip_w <= 0 || strip_w % 4 || w <= 0 || (w / 8) % strip_w) return DCT3D_EINVAL;
+    return encode_diag(c, d_raster, w, h, n_stacks, d_q, mode == 1 ? 4 : 5, nullptr, strip_w);
+}
+
+static int encode_diag(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int n_stacks, int32_t* d_q, int mode,
+                       uint64_t* d_trace, int strip_w) {
     CtxView v;
     if ((!d_raster || !d_q) && n_stacks) return DCT3D_EINVAL;
     int rc = view(c, v);
     uint64_t n_cubes = 0;
     if (rc || (rc = geometry(w, h, n_stacks, &n_cubes))) return rc;
-    if (mode != 1 && !((mode == 2 || mode == 3) && v.bd == 8)) return DCT3D_EINVAL;
+    if (mode != 1 && !((mode >= 2 && mode <= 5) && v.bd == 8)) return DCT3D_EINVAL;
     if (mode == 3 && !d_trace) return DCT3D_EINVAL;
     if (n_cubes == 0) return DCT3D_OK;
     EncodeParams P;
@@ -356,12 +369,19 @@ int dct3d_encode_trace_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, 
     P.width = (uint32_t)w;
     P.plane = (uint64_t)w * h;
     P.stack_stride = P.plane * v.bd;
+    if (strip_w) {
+        P.strip_w = (uint32_t)strip_w;
+        P.strip_cubes = (uint32_t)strip_w * (uint32_t)(h / 8);
+        P.div_strip_w = fast_div(P.strip_w);
+        P.div_strip_cubes = fast_div(P.strip_cubes);
+    }
     if (v.bd == 8) {  // the twins of encode16_kernel
         const uint32_t groups = (P.n_cubes + kE16CPW - 1) / kE16CPW;
         const dim3 grid((groups + kWavesPerBlock - 1) / kWavesPerBlock);
-        if (mode == 1) {
-            hipLaunchKernelGGL((encode16_kernel<true, 1>), grid, dim3(kBlock), 0, v.stream, P);
-        } else {  // compute only, with the product's tables
+        if (mode == 1 || mode == 4) {
+            if (mode == 1) hipLaunchKernelGGL((encode16_kernel<true, 1>), grid, dim3(kBlock), 0, v.stream, P);
+            else hipLaunchKernelGGL((encode16_kernel<true, 4>), grid, dim3(kBlock), 0, v.stream, P);
+        } else {  // compute only / the product with the strip traversal, with the product's tables
             const EncTables* t = enc8_tables(v.device);
             if (!t) return DCT3D_ENOMEM;
             P.coef_dc = t->coef_dc;
@@ -375,7 +395,8 @@ int dct3d_encode_trace_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, 
             P.group_of = t->group_of;
             P.trace = d_trace;
             if (mode == 2) hipLaunchKernelGGL((encode16_kernel<true, 2>), grid, dim3(kBlock), 0, v.stream, P);
-            else hipLaunchKernelGGL((encode16_kernel<true, 3>), grid, dim3(kBlock), 0, v.stream, P);
+            else if (mode == 3) hipLaunchKernelGGL((encode16_kernel<true, 3>), grid, dim3(kBlock), 0, v.stream, P);
+            else hipLaunchKernelGGL((encode16_kernel<true, 5>), grid, dim3(kBlock), 0, v.stream, P);
         }
     } else {
         const uint32_t groups = (P.n_cubes + kCubesPerWave - 1) / kCubesPerWave;

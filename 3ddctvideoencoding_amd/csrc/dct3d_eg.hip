@@ -379,75 +379,159 @@ __global__ __launch_bounds__(kEgBlock) void eg_compact_kernel(EgParams P, const 
 // in a true parse inside the wanted values that means a corrupt stream.
 constexpr uint64_t kChunkBits = kEgChunkBits;
 constexpr uint64_t kNoExit = ~0ull;
-// a block's window: its 256 chunks plus slack (a parse ends < 27 bits past its chunk; the reader's
-// buffer and the long-code path look < 96 bits ahead of its position); behind it the mark pass's dummies
-// (eg_mark_kernel: 2 bytes per thread)
-constexpr uint32_t kSyncWinWords = kEgBlock * (uint32_t)(kChunkBits / 32) + 8;
-constexpr uint32_t kSyncWinAlloc = kSyncWinWords + kEgBlock / 2;
 static_assert(kChunkBits == 512 && kEgBlock == 256, "16-word chunks");
 constexpr uint32_t kMarkVals = 32;          // values per emit lane / per mark
 constexpr uint32_t kEmitWinWords = 2048;    // per wave: window (<= 2,048 values x 27 bits) / 8 KiB staging
 
-__device__ __forceinline__ uint64_t chunk_start(const EgDecParams& P, uint64_t t, int iteration) {
-    if (t == 0) return P.start_bit;
-    if (iteration == 0) return P.start_bit + t * kChunkBits;
-    const uint64_t e = P.exit_in[t - 1];
-    return e == kNoExit ? P.start_bit + t * kChunkBits : e;
-}
+// ---------------------------------------------------------------------------------------------------------
+// The block's window as chunk columns (round 6).  A thread parses one 512-bit chunk; its reads wander over
+// its chunk, so in a linear window (rounds 1-5) the 32 lanes of a read's lane group sat 16 words apart on
+// 2 of the 32 banks of ds_read_b32 (MI355X_MICROARCH.md §LDS) until their offsets drifted apart: 6-8
+// conflict cycles per LDS instruction (profiles/r05/sq_c8_summary*.csv).  Column c of the window holds
+// chunk first + c shifted to start at bit 31 of its word 0, plus the first two words of the next chunk
+// (kColW words: every read of the lean and bounded steps), word j of column c at LDS word
+// (c / 32) * 32 kColW + 32 j + c % 32: a lane's reads all fall on bank c % 32, so a lane group's reads
+// never conflict, and word j of a column is one stride of 128 bytes from word j - 1, so the column read is
+// as cheap to address as a linear one (col_bits64).  Positions are chunk-relative 32-bit bits (0 = the
+// chunk's nominal first bit).  The rare checked steps that read past the column (a code of >= 33 bits
+// crossing the chunk end, the data's end) read the stream in global memory (ColReader).
+constexpr uint32_t kColW = 18;
+constexpr uint32_t kColBytes = kEgBlock * kColW * 4;
+static_assert(kEgBlock % 32 == 0, "whole lane groups of columns");
 
-// The block's window (chunks [first, first + kEgBlock) and 8 slack words), then a barrier.  Thread t
-// loads its own chunk's 16 words as four 16-byte loads (all in flight at once) and writes word j of it to
-// LDS as four 16-byte stores.  (Rounds 1-4: 17 coalesced dword loads per thread, thread i storing word
-// i + 256 b: the four 16-byte loads made the sync pass 422 -> 405 us, the mark pass 489 -> 471 us.)
-// Threads 0 and 1 also take the slack chunk's two quarters.  The data's last window (zeros past the
-// end) takes single predicated loads.
-__device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win, uint64_t first) {
+// LDS of the three front kernels, carved by hand so that the table sits right before the window (a
+// column's word -1, read and ignored by col_bits64 at p = 0, is then table bytes): table | window | ...
+constexpr uint32_t kLutBytes = 1u << 12;
+
+// The window of chunks first + c, c < kEgBlock (first may be -1: block 0 of the resolving pass), then the
+// caller's barrier.  Thread c loads its chunk's words (four 16-byte loads + three, all in flight at once),
+// funnel-shifts them by the stream's bit offset and writes them down its column.  Words past the stream
+// (or before it: chunk -1) are zero.
+__device__ __forceinline__ void stage_columns(const EgDecParams& P, uint32_t* win, int64_t first) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
-    const uint64_t w0 = (P.start_bit + first * kChunkBits) >> 5;
-    const uint32_t t = threadIdx.x;
-    const bool slack = t < 2;  // quarter t of the slack chunk (kEgBlock)
-    u32x4 v[5];
-    if (w0 + kSyncWinWords <= P.n_words) {  // block-uniform
-        const uint32_t* src = P.words + w0;
+    const int64_t b0 = (int64_t)P.start_bit + (first + (int64_t)threadIdx.x) * (int64_t)kChunkBits;
+    const int64_t w = b0 >> 5;  // arithmetic: floor
+    const uint32_t o = (uint32_t)b0 & 31u;  // the same for every chunk of the stream (block-uniform)
+    uint32_t g[kColW + 1];
+    if (w >= 0 && (uint64_t)w + kColW + 1 <= P.n_words) {
+        const uint32_t* src = P.words + w;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) v[q] = *(const u32x4*)(src + 16 * t + 4 * q);
-        v[4] = slack ? *(const u32x4*)(src + 16 * kEgBlock + 4 * t) : u32x4{0u, 0u, 0u, 0u};
+        for (int q = 0; q < 4; q++) {
+            const u32x4 x = *(const u32x4*)(src + 4 * q);
+            g[4 * q] = x[0]; g[4 * q + 1] = x[1]; g[4 * q + 2] = x[2]; g[4 * q + 3] = x[3];
+        }
+#pragma unroll
+        for (uint32_t j = 16; j <= kColW; j++) g[j] = src[j];
     } else {
 #pragma unroll
-        for (uint32_t q = 0; q < 5; q++) {
-            const uint64_t k0 = w0 + (q < 4 ? 16 * t + 4 * q : 16 * kEgBlock + 4 * t);
-#pragma unroll
-            for (uint32_t e = 0; e < 4; e++)
-                v[q][e] = k0 + e < P.n_words && (q < 4 || slack) ? P.words[k0 + e] : 0u;
+        for (uint32_t j = 0; j <= kColW; j++) {
+            const int64_t k = w + (int64_t)j;
+            g[j] = k >= 0 && (uint64_t)k < P.n_words ? P.words[k] : 0u;
         }
     }
 #pragma unroll
-    for (uint32_t q = 0; q < 4; q++)
-        *(uint4*)(win + 16 * t + 4 * q) = make_uint4(__builtin_bswap32(v[q][0]), __builtin_bswap32(v[q][1]),
-                                                     __builtin_bswap32(v[q][2]), __builtin_bswap32(v[q][3]));
-    if (slack)
-        *(uint4*)(win + 16 * kEgBlock + 4 * t) = make_uint4(__builtin_bswap32(v[4][0]), __builtin_bswap32(v[4][1]),
-                                                            __builtin_bswap32(v[4][2]), __builtin_bswap32(v[4][3]));
-    __syncthreads();
-    return LdsBits{win, w0, kSyncWinWords};
+    for (uint32_t j = 0; j <= kColW; j++) g[j] = __builtin_bswap32(g[j]);
+    uint32_t* col = win + (threadIdx.x >> 5) * (32 * kColW) + (threadIdx.x & 31);
+    if (o) {
+#pragma unroll
+        for (uint32_t j = 0; j < kColW; j++) col[32 * j] = __builtin_amdgcn_alignbit(g[j], g[j + 1], 32u - o);
+    } else {
+#pragma unroll
+        for (uint32_t j = 0; j < kColW; j++) col[32 * j] = g[j];
+    }
 }
-__device__ __forceinline__ LdsBits stage_block_window(const EgDecParams& P, uint32_t* win) {
-    return stage_block_window(P, win, (uint64_t)blockIdx.x * kEgBlock);
+__device__ __forceinline__ const uint32_t* column(const uint32_t* win) {
+    return win + (threadIdx.x >> 5) * (32 * kColW) + (threadIdx.x & 31);
 }
 
-// window-relative form of an absolute bit position (clamped: positions past the window behave as the
-// window's end, which only a limit or end beyond the window ever is)
-__device__ __forceinline__ uint32_t rel_bit(uint64_t p, uint64_t base) {
-    return p <= base ? 0u : (p - base >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(p - base));
+// chunk-relative form of an absolute bit position (clamped to [0, 2^32 - 1])
+__device__ __forceinline__ uint32_t rel_bit(uint64_t p, int64_t b0) {
+    if (b0 >= 0 && p <= (uint64_t)b0) return 0u;
+    const uint64_t d = p - (uint64_t)b0;
+    return d >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
 }
+
+// 32 stream bits at absolute bit a (MSB first; zero past the stream): the checked steps' rare global reads
+__device__ __forceinline__ uint32_t stream_bits32(const EgDecParams& P, uint64_t a) {
+    const uint64_t k = a >> 5;
+    const uint32_t o = (uint32_t)a & 31u;
+    const uint32_t x = stream_word(P, k), y = stream_word(P, k + 1);
+    return o ? __builtin_amdgcn_alignbit(x, y, 32u - o) : x;
+}
+
+// The buffered one-code-at-a-time reader of the checked steps (as BitReader, dct3d_eg_bits.h) over a column:
+// word i < kColW from LDS, beyond from the stream in global memory.
+struct ColReader {
+    const uint32_t* col;
+    const EgDecParams* P;
+    uint64_t b0;     // absolute bit of the column's bit 0 (a live chunk: >= 0)
+    uint32_t next;   // index of the word held in `pre`
+    uint64_t buf;    // left-aligned bits [pos, pos + avail)
+    int avail;
+    uint32_t pos;
+    uint32_t pre;
+    __device__ __forceinline__ uint32_t word(uint32_t i) const {
+        if (i < kColW) return col[32 * i];
+        return stream_bits32(*P, b0 + 32ull * i);
+    }
+    __device__ __forceinline__ void seek(uint32_t p) {
+        pos = p;
+        const uint32_t k = p >> 5;
+        const int sh = (int)(p & 31);
+        buf = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+        avail = 64 - sh;
+        next = k + 2;
+        pre = word(next);
+    }
+    __device__ __forceinline__ void refill() {
+        if (avail <= 32) {
+            buf |= (uint64_t)pre << (32 - avail);
+            avail += 32;
+            pre = word(++next);
+        }
+    }
+    // a run of 1-bit codes (value 0), at most maxn, stopping where the buffered bits end
+    __device__ __forceinline__ uint32_t ones(uint32_t maxn) {
+        refill();
+        const uint64_t inv = ~buf;
+        uint32_t n1 = inv ? (uint32_t)__clzll((long long)inv) : 64u;
+        n1 = min(min(n1, (uint32_t)avail), maxn);
+        buf = n1 >= 64 ? 0ull : buf << n1;
+        avail -= (int)n1;
+        pos += n1;
+        return n1;
+    }
+    __device__ __forceinline__ bool at_long_code() const { return avail > 0 && !(buf >> 63); }
+    // one codeword (any width up to 63 bits): false when 32 zero bits come first (invalid)
+    __device__ __forceinline__ bool get(uint32_t& code) {
+        refill();
+        const uint32_t hi32 = (uint32_t)(buf >> 32);
+        if (hi32 == 0u) return false;
+        const int width = 2 * __builtin_clz(hi32) + 1;
+        if (width <= avail) {
+            code = (uint32_t)(buf >> (64 - width));
+            buf <<= width;
+            avail -= width;
+            pos += (uint32_t)width;
+        } else {  // a long code straddling the buffer: read it at its position
+            const uint32_t k = pos >> 5;
+            const int sh = (int)(pos & 31);
+            const uint64_t hi = (((uint64_t)word(k) << 32) | word(k + 1)) << sh;
+            const uint64_t x = sh ? (hi | ((uint64_t)word(k + 2) >> (32 - sh))) : hi;
+            code = (uint32_t)(x >> (64 - width));
+            seek(pos + (uint32_t)width);
+        }
+        return true;
+    }
+};
 
 // A parse from a wrong start meets the true parse (a boundary of both) within 90 bits on every one of
 // 10.7 k chunks of the 1080p content (within 64 bits on 99.57 %, at the chunk start on half of them).
 constexpr uint32_t kMeetBits = 128;
 
-// One parse step (a run of 1-bit codes, or one longer code): false once the parse has ended (at
+// One checked parse step (a run of 1-bit codes, or one longer code): false once the parse has ended (at
 // `stop`, or invalid).
-__device__ __forceinline__ bool sync_step(WinReader& r, uint32_t stop, uint32_t limit, uint32_t& n, bool& invalid) {
+__device__ __forceinline__ bool sync_step(ColReader& r, uint32_t stop, uint32_t limit, uint32_t& n, bool& invalid) {
     uint32_t code;
     const uint32_t k = r.ones(min(stop - r.pos, 64u));
     n += k;
@@ -461,96 +545,45 @@ __device__ __forceinline__ bool sync_step(WinReader& r, uint32_t stop, uint32_t 
     return true;
 }
 
-// The parse passes' chunk interiors: a branchless step (round 4).  The interior loops of round 3 branched
-// per step (refill, run marks, long code, code mark); every branch is exec-mask bookkeeping on the scalar
-// unit and a wave ran each branch any of its lanes took.  Measured (c8, one box, A/B x 2): sync 625 ->
-// 558 us, mark 896 -> 798 us.  Two chunks per thread interleaved through the same step ran slower (739 /
-// 961 us: half the waves, and the compiler did not interleave the chains), not kept.
-// WinReader's state inside a chunk's interior as 32-bit words: bits [pos, pos + avail) left-aligned in
-// hi:lo and zero past avail, the word after them (index nx) in pre; pos = 32 nx - avail.
-struct Lean {
-    uint32_t hi, lo, avail, nx, pre;
-    __device__ __forceinline__ uint32_t pos() const { return nx * 32u - avail; }
-};
-__device__ __forceinline__ Lean lean_from(const WinReader& r) {
-    return Lean{(uint32_t)(r.buf >> 32), (uint32_t)r.buf, (uint32_t)r.avail, r.next, r.pre};
+// The parse passes' chunk interiors: branchless steps read from the column at their position (round 6).
+// Round 4 made the interior steps branchless (sync 625 -> 558 us, mark 896 -> 798 us per c8 step: every
+// branch was exec-mask bookkeeping on the scalar unit that a wave ran whenever any lane took it); rounds 4-5
+// carried a 64-bit buffer with its fill count and a one-word prefetch between steps, so every step paid a
+// select-based refill (~10 VALU of 33 in the sync pass's table step).  Now a step carries only its position
+// p and reads the 64 bits at p from its column -- words k - 1 .. k + 1, k = ceil(p / 32), two funnel
+// shifts by (32 - p mod 32) mod 32 (the consumer's parse_step, dct3d_eg_bits.h): no refill, no fill count,
+// no carried words; its LDS read sits on the step's dependent chain, conflict-free in the column layout.
+__device__ __forceinline__ void col_bits64(const uint32_t* col, uint32_t p, uint32_t& hi, uint32_t& lo) {
+    const int32_t n = -(int32_t)p;
+    const uint32_t* w = (const uint32_t*)((const char*)col + __mul24(n >> 5, -128));
+    const uint32_t x0 = w[-32], x1 = w[0], x2 = w[32];
+    hi = __builtin_amdgcn_alignbit(x0, x1, (uint32_t)n);  // alignbit reads the shift's low 5 bits only
+    lo = __builtin_amdgcn_alignbit(x1, x2, (uint32_t)n);
 }
-__device__ __forceinline__ void lean_to(WinReader& r, const Lean& c) {
-    r.buf = ((uint64_t)c.hi << 32) | c.lo;
-    r.avail = (int)c.avail;
-    r.next = c.nx;
-    r.pos = c.pos();
-    r.pre = r.s[c.nx < r.n ? c.nx : 0u];
+// leading zeros of x, 0xFFFFFFFF for x = 0 (the hardware's v_ffbh_u32; clz(0) is undefined in C++, and a
+// zero top word means an invalid code here: >= 16 as an unsigned count)
+__device__ __forceinline__ uint32_t ffbh_u32(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
 }
 
-// The window word reader of the lean steps (a functor: the interior loops were measured with other window
-// layouts)
-struct WinRead {
-    const uint32_t* s;
-    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return s[i]; }
-};
-
-// One branchless step inside the interior (every word read lies in the window): a run of 1-bit codes
-// (value 0) of up to 31 -- a run never extends past avail, whose bits are zero -- then a refill to >= 32
-// bits, then the longer code that follows the run if there is one.  Returns the values taken (<= 32);
-// bad: that code has >= 33 bits or 32 leading zeros (left unconsumed for the checked loop).  A run cut
-// short by avail takes no code; the next step continues it.  BOUNDED: room (>= 1) bits are left before
-// the parse's stop; the run ends there at the latest and a code is taken only if it starts before it,
-// so the parse ends exactly at the first code boundary at or past the stop (the code may reach past).
-// CAP: the run's cap when unbounded (31).  n1_out / w_out: the run's length and the code's width (0: none).
-template <bool BOUNDED = false, uint32_t CAP = 31u, class Rd>
-__device__ __forceinline__ uint32_t lean_step(const Rd& s, Lean& c, bool& bad, uint32_t room = 32u,
-                                              uint32_t* n1_out = nullptr, uint32_t* w_out = nullptr) {
-    // ones at the top of hi, at most CAP (BOUNDED: at most room): the OR-ed bit makes clz defined and caps it
-    const uint32_t cap_bit = BOUNDED ? 0x80000000u >> min(room, 31u) : 0x80000000u >> CAP;
-    uint32_t n1 = __builtin_clz(~c.hi | cap_bit);
-    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
-    c.avail -= n1;
-    // a 0 bit follows the run: a code starts (BOUNDED: before the stop)
-    const bool has = c.avail != 0u && (uint32_t)(b >> 63) == 0u && (!BOUNDED || n1 < room);
-    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
-    // refill: append pre when fewer than 32 bits are buffered (branchless; the re-read of pre is
-    // unconditional, the same word when nothing was appended)
-    const bool need = c.avail < 32u;
-    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
-    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);  // pre << (32 - avail); 0 at avail 0
-    hi = need ? rh : hi;
-    lo = need ? rl : lo;
-    c.avail += need ? 32u : 0u;
-    c.nx += need ? 1u : 0u;
-    c.pre = s(c.nx);
-    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
-    bad = has && zz >= 16u;
-    const bool take = has && zz < 16u;
-    const uint32_t w = take ? 2u * zz + 1u : 0u;
-    b = (((uint64_t)hi << 32) | lo) << w;
-    c.hi = (uint32_t)(b >> 32);
-    c.lo = (uint32_t)b;
-    c.avail -= w;
-    if (n1_out) *n1_out = n1;
-    if (w_out) *w_out = w;
-    return n1 + (take ? 1u : 0u);
-}
-// The interior loops run while the parse is a margin short of every bound.  A step's reads past the bound
-// stay inside the block window (the last chunk's bound has the 256-bit slack behind it), so only the bits
-// a step takes must stay short of it: the table steps of both passes take <= 31 + 31 bits; the bounded
-// steps then finish the chunk.  (128, the window-read bound, before: sync 346 -> 311 us, mark 464 -> 442
-// us per c8 step with its former two-code step, A/B x 3 on one box, profiles/r05/c8_ab.)
+// The interior loops run while the parse is a margin short of every bound: a step takes at most 31 + 31
+// bits (a run of <= 31 one-bit codes, then the table's <= 12 bits or one code of <= 31), so only those
+// bits must stay short of the bound.  Interior steps (p < 512 - 64) read words <= 15, the bounded steps
+// (p < 512) words <= 17: the column.  (Round 5: 128, the old window-read bound, before: sync 346 -> 311
+// us, mark 464 -> 442 us per c8 step.)
 constexpr uint32_t kLeanMargin = 64;
-static_assert(31 + 31 < kLeanMargin && 31 * 8 < 256, "steps stay short of the bound");
+static_assert(31 + 31 < kLeanMargin && (kChunkBits + 31) / 32 + 1 < kColW, "steps stay in the column");
 
-// Sync-pass step by table (round 5): a run of 1-bit codes as lean_step, a refill to >= 32 bits, then every
-// code that lies wholly in the next kEgLutBits bits at once, from a 4 KiB table of (codes, bits) per bit
-// pattern; no code complete in them (a code of more than kEgLutBits bits): one code by its leading zeros.
-// A step moves at most 31 + 31 bits (kLeanMargin).  The sync pass needs only the count and the exit, so the
-// codes' individual boundaries are never formed.
-// Table width of the mark pass (12: 4 KiB, 5 blocks per CU beside its window and mark slots) and of the
-// sync pass (DCT3D_SYNC_LUT_BITS, default 12: 7 blocks per CU)
+// Table step: a run of 1-bit codes (clz of the complement, at most 31), then every code complete in the
+// next kEgLutBits bits at once from a 4 KiB LDS table of (codes, bits) per bit pattern; none complete (a
+// code of more than kEgLutBits bits): one code by its leading zeros.  20 VALU (round 5's buffered form:
+// 33).  The sync pass needs only the count and the exit, so the codes' boundaries are never formed.
+// Table width 12 bits: a 13- or 14-bit sync table cost more blocks per CU than it saved, a 10- or 11-bit
+// mark table took more steps (profiles/r05/sync_table_bits, mark_table_bits).
 constexpr int kEgLutBits = 12;
-#ifndef DCT3D_SYNC_LUT_BITS
-#define DCT3D_SYNC_LUT_BITS 12
-#endif
-constexpr int kSyncLutBits = DCT3D_SYNC_LUT_BITS;
+static_assert((1u << kEgLutBits) == kLutBytes, "the carved table");
 template <int B>
 struct EgLut {
     uint8_t e[1 << B];  // codes complete within the pattern (low 4 bits), the bits they take (high 4)
@@ -572,121 +605,236 @@ constexpr EgLut<B> make_eg_lut() {
     return t;
 }
 __device__ constexpr EgLut<kEgLutBits> kEgLut = make_eg_lut<kEgLutBits>();
-__device__ constexpr EgLut<kSyncLutBits> kSyncLut = make_eg_lut<kSyncLutBits>();
-// the block's copy of a table: 16-byte pieces, ordered by the staging's barrier
-template <int B>
-__device__ __forceinline__ void copy_lut(uint8_t* s_lut, const EgLut<B>& t) {
-    static_assert((1 << B) % (16 * kEgBlock) == 0, "whole 16-byte pieces per thread");
+// the block's copy of the table: 16-byte pieces, ordered by the staging's barrier
+__device__ __forceinline__ void copy_lut(uint8_t* s_lut) {
+    static_assert(kLutBytes % (16 * kEgBlock) == 0, "whole 16-byte pieces per thread");
 #pragma unroll
-    for (int r = 0; r < (1 << B) / (16 * kEgBlock); r++)
-        *(uint4*)(s_lut + 16 * (threadIdx.x + r * kEgBlock)) = *(const uint4*)(t.e + 16 * (threadIdx.x + r * kEgBlock));
+    for (uint32_t r = 0; r < kLutBytes / (16 * kEgBlock); r++)
+        *(uint4*)(s_lut + 16 * (threadIdx.x + r * kEgBlock)) = *(const uint4*)(kEgLut.e + 16 * (threadIdx.x + r * kEgBlock));
 }
-static_assert(kEgLutBits <= 15 && kSyncLutBits <= 15, "counts and widths fit 4 bits");
+static_assert(kEgLutBits <= 15, "counts and widths fit 4 bits");
 
-template <int B, class Rd>
-__device__ __forceinline__ uint32_t lean_step_lut(const Rd& s, const uint8_t* lut, Lean& c, bool& bad) {
-    const uint32_t n1 = __builtin_clz(~c.hi | 1u);  // run of 1-bit codes, at most 31, never past avail
-    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
-    c.avail -= n1;
-    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
-    const bool need = c.avail < 32u;  // refill (as lean_step): the run ended on a code boundary either way
-    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
-    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);
-    hi = need ? rh : hi;
-    lo = need ? rl : lo;
-    c.avail += need ? 32u : 0u;
-    c.nx += need ? 1u : 0u;
-    c.pre = s(c.nx);
-    const uint32_t e = lut[hi >> (32 - B)];
+// A step that meets a code of >= 33 bits (or 32 zero bits) ends the interior loop with that code counted
+// and its (meaningless) width added to p; the loop's caller takes both back (pos_step_undo), so the step
+// needs no selects for the case.
+__device__ __forceinline__ uint32_t pos_step_lut(const uint32_t* col, const uint8_t* lut, uint32_t& p, bool& bad,
+                                                 uint32_t& w_last) {
+    uint32_t hi, lo;
+    col_bits64(col, p, hi, lo);
+    const uint32_t n1 = __builtin_clz(~hi | 1u);  // run of 1-bit codes, at most 31
+    const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
+    const uint32_t e = lut[th >> (32 - kEgLutBits)];
     const uint32_t k = e & 15u;
-    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
-    const bool one = k == 0u && zz < 16u;  // one code of 13 .. 31 bits
-    bad = k == 0u && zz >= 16u;            // >= 33 bits or invalid: the checked loop reads it
-    const uint32_t w = k ? e >> 4 : (one ? 2u * zz + 1u : 0u);
-    b = (((uint64_t)hi << 32) | lo) << w;
-    c.hi = (uint32_t)(b >> 32);
-    c.lo = (uint32_t)b;
-    c.avail -= w;
-    return n1 + (k ? k : (one ? 1u : 0u));
+    const uint32_t zz = ffbh_u32(th);
+    const bool kz = k == 0u;                 // no code complete in the table's bits: one code by clz
+    bad = kz & (zz >= 16u);                  // >= 33 bits or invalid: the checked loop reads it
+    w_last = kz ? 2u * zz + 1u : e >> 4;
+    p += n1 + w_last;
+    return n1 + max(k, 1u);
+}
+__device__ __forceinline__ void pos_step_undo(bool bad, uint32_t w_last, uint32_t& p, uint32_t& n) {
+    if (bad) {  // the code the last step met: back to its first bit, uncounted
+        p -= w_last;
+        n -= 1u;
+    }
 }
 
-// The mark pass's table step: lean_step_lut that stops on the step's one possible mark.  d0: the values
+// The mark pass's table step: pos_step_lut that stops on the step's one possible mark.  d0: the values
 // before the next mark.  All k table codes are taken unless the step's values would pass 32 (two marks) or
 // the mark falls on the table's second .. k-th code, whose bit offsets the table does not give; then only
 // the first code (its width by clz).  The mark is then always the run's d0-th value or the first code: bit
-// p0 + d0 of the step.  A step moves at most 31 + 31 bits.  (Round 5: the two-code step before it -- a run
-// of <= 30, a code, a second code when buffered, 53 VALU with the mark -- against 46 VALU and 9 % / 25 %
-// fewer steps on ramp / uniform content: the pass 430 -> 356 us per c8 step although its 4 KiB table costs
-// a sixth block per CU, profiles/r05/mark_lut.)
-template <class Rd>
-__device__ __forceinline__ uint32_t lean_step_lut_mark(const Rd& s, const uint8_t* lut, Lean& c, bool& bad,
-                                                       uint32_t d0) {
-    const uint32_t n1 = __builtin_clz(~c.hi | 1u);
-    uint64_t b = (((uint64_t)c.hi << 32) | c.lo) << n1;
-    c.avail -= n1;
-    uint32_t hi = (uint32_t)(b >> 32), lo = (uint32_t)b;
-    const bool need = c.avail < 32u;
-    const uint32_t rh = hi | (c.pre >> (c.avail & 31u));
-    const uint32_t rl = __builtin_amdgcn_alignbit(c.pre, 0u, c.avail);
-    hi = need ? rh : hi;
-    lo = need ? rl : lo;
-    c.avail += need ? 32u : 0u;
-    c.nx += need ? 1u : 0u;
-    c.pre = s(c.nx);
-    const uint32_t e = lut[hi >> (32 - kEgLutBits)];
+// p0 + d0 of the step.  (Round 5: the table in the mark pass, 430 -> 356 us per c8 step, profiles/r05/mark_lut.)
+__device__ __forceinline__ uint32_t pos_step_lut_mark(const uint32_t* col, const uint8_t* lut, uint32_t& p, bool& bad,
+                                                      uint32_t d0, uint32_t& w_last) {
+    uint32_t hi, lo;
+    col_bits64(col, p, hi, lo);
+    const uint32_t n1 = __builtin_clz(~hi | 1u);
+    const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
+    const uint32_t e = lut[th >> (32 - kEgLutBits)];
     const uint32_t k = e & 15u;
-    const uint32_t zz = hi ? (uint32_t)__builtin_clz(hi) : 32u;
-    const bool full = k != 0u && n1 + k <= 32u && d0 - n1 - 1u >= k - 1u;
-    const bool one = !full && zz < 16u;
-    bad = !full && zz >= 16u;
-    const uint32_t w = full ? e >> 4 : (one ? 2u * zz + 1u : 0u);
-    b = (((uint64_t)hi << 32) | lo) << w;
-    c.hi = (uint32_t)(b >> 32);
-    c.lo = (uint32_t)b;
-    c.avail -= w;
-    return n1 + (full ? k : (one ? 1u : 0u));
+    const uint32_t zz = ffbh_u32(th);
+    // (bitwise, not short-circuit: the compiler made branches of &&)
+    const bool full = (k != 0u) & (n1 + k <= 32u) & (d0 - n1 - 1u >= k - 1u);
+    bad = !full & (zz >= 16u);  // counted and taken back by the caller (pos_step_undo), as pos_step_lut
+    const uint32_t wt = e >> 4, w1 = 2u * zz + 1u;
+    w_last = full ? wt : w1;
+    p += n1 + w_last;
+    return n1 + (full ? k : 1u);
 }
 
-// The resolve walk of chunk t (pass 0 with resolve, below): e = the pass-0 exit of chunk t - 1 (~0u: it
-// ended invalid), s0 = chunk t's pass-0 start, x0 = its pass-0 exit (window-relative), n = its pass-0
-// count, ex = its pass-0 exit (absolute).  On return n / exit are chunk t's true count and exit; true
-// (fail) when the true exit differs from the pass-0 exit that chunk t + 1 was resolved against.
-__device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, uint32_t s0, uint32_t x0, uint32_t stop,
-                                              uint32_t limit, uint64_t base, uint64_t ex, uint32_t& n, uint64_t& exit) {
-    if (e == ~0u) return false;
-    bool met = false;
-    if (e - s0 < kMeetBits) {  // e >= s0: the exit of chunk t - 1 lies at or past its end
-        WinReader a{win, kSyncWinWords, 0, 0, 0, 0, 0};  // pass 0, from s0
-        WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};  // the true parse, from e
-        a.seek(s0);
-        q.seek(e);
-        uint32_t na = 0, nq = 0, code;
-        for (;;) {
-            if (a.pos == q.pos) {  // met: a boundary of both parses
-                met = a.pos <= x0;  // ... at or before the pass-0 exit (else: past the data's end)
-                if (met) n = n - na + nq;
-                break;
-            }
-            if (min(a.pos, q.pos) - s0 >= kMeetBits || max(a.pos, q.pos) > limit) break;
-            const bool adv_a = a.pos < q.pos;  // the one behind takes its next code
-            if (!(adv_a ? a.get(code) : q.get(code))) break;  // 32 zero bits
-            if (adv_a) na++;
-            else nq++;
+// Bounded table steps to the chunk end (round 6; rounds 4-5 took one run and one code per bounded step,
+// ~9 steps over the last 64 bits of ramp content): the run is capped at the bits left before the stop, the
+// table's codes are taken when they all end at or before it (no code boundary at or past the stop is
+// skipped), else the one code after the run if it starts before the stop.  So the parse still ends
+// exactly at the first code boundary at or past the stop.  bad: as pos_step_lut, but the code is left
+// unconsumed (the checked loop reads it).
+__device__ __forceinline__ uint32_t pos_step_lut_bounded(const uint32_t* col, const uint8_t* lut, uint32_t& p, bool& bad,
+                                                         uint32_t stop) {
+    const uint32_t room = stop - p;
+    uint32_t hi, lo;
+    col_bits64(col, p, hi, lo);
+    const uint32_t n1 = __builtin_clz(~hi | (0x80000000u >> min(room, 31u)));
+    const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
+    const uint32_t e = lut[th >> (32 - kEgLutBits)];
+    const uint32_t k = e & 15u, wt = e >> 4;
+    const uint32_t zz = ffbh_u32(th);
+    const bool has = ((th >> 31) == 0u) & (n1 < room);  // a code starts after the run, before the stop
+    const bool table = has & (k != 0u) & (p + n1 + wt <= stop);
+    const bool one = has & !table;
+    bad = one & (zz >= 16u);
+    const bool take1 = one & (zz < 16u);
+    p += n1 + (table ? wt : (take1 ? 2u * zz + 1u : 0u));
+    return n1 + (table ? k : (take1 ? 1u : 0u));
+}
+// ... and with the mark pass's one-mark rule (pos_step_lut_mark)
+__device__ __forceinline__ uint32_t pos_step_lut_mark_bounded(const uint32_t* col, const uint8_t* lut, uint32_t& p,
+                                                              bool& bad, uint32_t d0, uint32_t stop) {
+    const uint32_t room = stop - p;
+    uint32_t hi, lo;
+    col_bits64(col, p, hi, lo);
+    const uint32_t n1 = __builtin_clz(~hi | (0x80000000u >> min(room, 31u)));
+    const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
+    const uint32_t e = lut[th >> (32 - kEgLutBits)];
+    const uint32_t k = e & 15u, wt = e >> 4;
+    const uint32_t zz = ffbh_u32(th);
+    const bool has = ((th >> 31) == 0u) & (n1 < room);
+    const bool full = has & (k != 0u) & (n1 + k <= 32u) & (d0 - n1 - 1u >= k - 1u) & (p + n1 + wt <= stop);
+    const bool one = has & !full;
+    bad = one & (zz >= 16u);
+    const bool take1 = one & (zz < 16u);
+    p += n1 + (full ? wt : (take1 ? 2u * zz + 1u : 0u));
+    return n1 + (full ? k : (take1 ? 1u : 0u));
+}
+
+// Pass-0 / confirming parse of a chunk from chunk-relative bit s to its end (stop = min(512, limit)):
+// exactly the codes a one-at-a-time parse reads (every 1-bit code boundary is a code boundary).  The
+// interior by table steps without bounds, then the bounded steps to the chunk end, then (only if a long or
+// invalid code or the data's end stopped them) the checked steps.  Returns the count; *pos = the exit.
+__device__ __forceinline__ uint32_t parse_chunk(const EgDecParams& P, const uint32_t* col, const uint8_t* lut, int64_t b0,
+                                                uint32_t s, uint32_t stop, uint32_t limit, uint32_t& pos, bool& invalid) {
+    const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
+    // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the chunk
+    // end (a code running past the limit is invalid: the checked steps)
+    const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
+    uint32_t p = s, n = 0, w_last = 0;
+    bool bad = false;
+    while (!bad & (p < fast_stop)) n += pos_step_lut(col, lut, p, bad, w_last);
+    pos_step_undo(bad, w_last, p, n);
+    while (!bad & (p < bstop)) n += pos_step_lut_bounded(col, lut, p, bad, bstop);
+    invalid = false;
+    if (p < stop) {
+        ColReader r{col, &P, (uint64_t)b0, 0, 0, 0, 0, 0};
+        r.seek(p);
+        while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
+        }
+        p = r.pos;
+    }
+    pos = p;
+    return n;
+}
+
+// The resolve walk (pass 0 with resolve, below), chunk-relative: the pass-0 parse of a chunk (a, from its
+// first bit) and its true parse (q, from e, the pass-0 exit of the chunk before) are walked until they
+// stand on the same bit.  Branch-free steps of the parse behind, read from the column (round 6; rounds 1-5
+// took one code per iteration through two buffered readers).  Invariant: every boundary the parse ahead
+// visited before its current position lies at or behind the parse behind (it moved only while behind), so
+// the next common boundary is at or past `ahead`.  Hence the parse behind may take (a) a run of 1-bit codes
+// -- every bit of it a boundary, so a run reaching `ahead` meets there -- and (b) all codes the table sees
+// complete when they end at or before `ahead`, else one code.  A code of >= 33 bits or 32 zero bits ends
+// the walk unmet (stuck: the confirming parse).
+struct Walk {
+    uint32_t pa, pq, na, nq;
+    bool stuck;
+};
+__device__ __forceinline__ bool walk_done(const Walk& w, uint32_t limit) {
+    return w.pa == w.pq || min(w.pa, w.pq) >= kMeetBits || max(w.pa, w.pq) > limit || w.stuck;
+}
+// up to `steps` steps (the ended lanes idle); true when the walk has ended
+__device__ __forceinline__ bool walk(const uint32_t* col, const uint8_t* lut, uint32_t limit, Walk& w, uint32_t steps) {
+    for (uint32_t i = 0; i < steps && !walk_done(w, limit); i++) {
+        const bool a_behind = w.pa < w.pq;
+        const uint32_t behind = min(w.pa, w.pq), ahead = max(w.pa, w.pq);
+        uint32_t hi, lo;
+        col_bits64(col, behind, hi, lo);
+        const uint32_t n1 = __builtin_clz(~hi | 1u);  // <= 31
+        const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
+        const uint32_t ent = lut[th >> (32 - kEgLutBits)];
+        const uint32_t k = ent & 15u, wt = ent >> 4;
+        const uint32_t zz = ffbh_u32(th);
+        const bool run_meet = behind + n1 >= ahead;
+        const bool code = (th >> 31) == 0u;  // a code follows the run (not a capped run)
+        const bool table = (k != 0u) & (behind + n1 + wt <= ahead);
+        w.stuck = !run_meet & !table & code & (zz >= 16u);
+        const uint32_t adv = w.stuck ? 0u : (run_meet ? ahead - behind : n1 + (table ? wt : (code ? 2u * zz + 1u : 0u)));
+        const uint32_t cnt = run_meet ? ahead - behind : n1 + (table ? k : (code ? 1u : 0u));
+        w.pa += a_behind ? adv : 0u;
+        w.na += a_behind && adv ? cnt : 0u;
+        w.pq += a_behind ? 0u : adv;
+        w.nq += !a_behind && adv ? cnt : 0u;
+    }
+    return walk_done(w, limit);
+}
+
+// The resolve of a block's chunks (every thread calls it: it holds two barriers).  own: the thread's chunk
+// is the block's (not the helper, not past the data); e: its true start as far as pass 0 knows it (the
+// pass-0 exit of the chunk before, chunk-relative; 0 for chunk 0; ~0u: that parse ended invalid, which a
+// confirming pass would repeat from the nominal start: nothing to resolve); x0 / inv0 / n: its pass-0 exit
+// and count.  Returns fail (the true exit differs from the pass-0 exit the next chunk was resolved
+// against); n / x: the true count and exit (~0u: invalid).
+// Walk lengths are short on average but long-tailed (1080p ramp content: mean 1.1 steps, 99th percentile
+// 15; the maximum over a wave's 63 chunks averages 15 -- tools/walk_sim.py), and a wave runs as long as its
+// longest walk.  So each lane takes kWalkSimt steps, then the walks still going (~10 % on ramp content)
+// are queued in LDS and finished by wave 0, 64 at a time: a block pays the long tail once instead of once
+// per wave (simulated: 59 -> 26 wave-steps per block on ramp content, 71 -> 30 on uniform noise).
+constexpr uint32_t kWalkSimt = 2;
+__device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32_t* win, const uint8_t* lut,
+                                              uint32_t* s_q, uint32_t* s_qn, int64_t first, bool own, uint32_t e,
+                                              uint32_t x0, bool inv0, uint32_t stop, uint32_t limit, int64_t b0,
+                                              uint32_t& n, uint32_t& x) {
+    const uint32_t* col = column(win);
+    x = inv0 ? ~0u : x0;
+    const bool walking = own && e < kMeetBits;  // (e = ~0u: not walking)
+    Walk w{0u, walking ? e : 0u, 0u, 0u, false};
+    uint32_t slot = ~0u;
+    if (walking && !walk(col, lut, limit, w, kWalkSimt)) {
+        slot = atomicAdd(s_qn, 1u);
+        s_q[2 * slot] = threadIdx.x | (w.pa << 8) | (w.pq << 16) | (w.na << 24);  // all < 256
+        s_q[2 * slot + 1] = w.nq;
+    }
+    __syncthreads();
+    const uint32_t qn = *s_qn;
+    if (threadIdx.x < 64) {
+        for (uint32_t i = threadIdx.x; i < qn; i += 64) {
+            const uint32_t a = s_q[2 * i];
+            const uint32_t c = a & 255u;
+            Walk v{(a >> 8) & 255u, (a >> 16) & 255u, a >> 24, s_q[2 * i + 1], false};
+            const int64_t bc = (int64_t)P.start_bit + (first + (int64_t)c) * (int64_t)kChunkBits;
+            (void)walk(win + (c >> 5) * (32 * kColW) + (c & 31), lut, rel_bit(P.limit_bit, bc), v, ~0u);
+            s_q[2 * i] = c | (v.pa << 8) | (v.pq << 16) | (v.na << 24);
+            s_q[2 * i + 1] = v.nq | (v.stuck ? 0x80000000u : 0u);
         }
     }
-    if (met) return false;
-    // rare (a dense run of long codes): the confirming pass of this chunk, inline
-    WinReader q{win, kSyncWinWords, 0, 0, 0, 0, 0};
-    q.seek(e);
-    uint32_t n2 = 0;
-    bool inv2 = false;
-    while (q.pos < stop && sync_step(q, stop, limit, n2, inv2)) {
+    __syncthreads();
+    if (slot != ~0u) {
+        const uint32_t a = s_q[2 * slot], c = s_q[2 * slot + 1];
+        w = Walk{(a >> 8) & 255u, (a >> 16) & 255u, a >> 24, c & 0x7FFFFFFFu, (c >> 31) != 0u};
     }
-    n = n2;
-    exit = inv2 ? kNoExit : base + q.pos;
-    // chunk t + 1 was resolved against the pass-0 exit: only a different true exit needs the confirming
+    if (!own || e == ~0u) return false;
+    if (walking && w.pa == w.pq && w.pa <= x0) {  // met at or before the pass-0 exit (else: past the data)
+        n = n - w.na + w.nq;
+        return false;
+    }
+#ifdef DCT3D_DIAG_NO_CONFIRM  // diagnostic build: the walk without the confirming parse (timing only)
+    return false;
+#endif
+    // rare (a dense run of long codes): the confirming pass of this chunk, inline
+    bool inv2 = false;
+    uint32_t x2 = 0;
+    n = parse_chunk(P, col, lut, b0, e, stop, limit, x2, inv2);
+    x = inv2 ? ~0u : x2;
+    // the next chunk was resolved against the pass-0 exit: only a different true exit needs the confirming
     // passes
-    return exit != ex;
+    return x != (inv0 ? ~0u : x0);
 }
 
 // Sync pass.  resolve (pass 0 only): the block owns kEgBlock - 1 chunks, [b * 255, b * 255 + 255), on
@@ -701,47 +849,59 @@ __device__ __forceinline__ bool resolve_chunk(const uint32_t* win, uint32_t e, u
 // ended invalid, a confirming pass would restart chunk t at its nominal start, i.e. repeat pass 0: met.)
 // A chunk whose parses do not meet within kMeetBits runs its own confirming parse from e through the
 // chunk, in place; only if that exit differs from the pass-0 exit (which chunk t + 1 resolved against)
-// is status[0] set, and the host then runs confirming passes (iteration 1, plain mapping).
-__global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
-    __shared__ uint32_t win[kSyncWinAlloc];
-    __shared__ uint32_t s_exit[kEgBlock];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kSyncLutBits];
-    copy_lut(s_lut, kSyncLut);
+// is status[0] set, and the host then runs confirming passes (iteration 1, plain mapping).  The fused
+// front (eg_front_kernel) runs this pass, the scan and the mark pass in one launch; these kernels are its
+// non-speculative rerun and the DCT3D_OPT_EG_NO_RESOLVE path.
+// DIAG (diagnostic builds, DCT3D_DIAG_FRONT, timing only): 1 = the staging alone, 2 = + the pass-0
+// interior loop, 3 = + the whole pass-0 parse, 4 = + the barrier and the exits in LDS, 5 = + the resolve
+// walk (no stores); nothing is written
+template <int DIAG>
+__device__ __forceinline__ void sync_body(const EgDecParams& P, int iteration, int resolve) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + 3 * kEgBlock + 1];
+    uint8_t* const s_lut = (uint8_t*)lds;
+    uint32_t* const win = lds + kLutBytes / 4;
+    uint32_t* const s_exit = win + kColBytes / 4;
+    uint32_t* const s_q = s_exit + kEgBlock;  // the resolve's walk queue (resolve_block), its count after it
+    uint32_t* const s_qn = s_q + 2 * kEgBlock;
+    copy_lut(s_lut);
+    if (threadIdx.x == 0) *s_qn = 0u;
     const bool rs = iteration == 0 && resolve;
-    const uint64_t b = blockIdx.x;
-    const uint64_t first = rs ? (b ? b * (kEgBlock - 1) - 1 : 0) : b * kEgBlock;
-    const LdsBits L = stage_block_window(P, win, first);
-    // rs: block 0's thread 0 has no helper chunk (t = -1 wraps: past n_chunks)
-    const uint64_t t = rs ? b * (kEgBlock - 1) + threadIdx.x - 1 : first + threadIdx.x;
-    const bool live = t < P.n_chunks;
-    const uint64_t base = L.w0 * 32;
-    const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
-    const uint32_t limit = rel_bit(P.limit_bit, base);
-    const uint32_t stop = min(end, limit);
-    WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
-    const uint32_t s0 = live ? rel_bit(chunk_start(P, t, iteration), base) : 0u;
-    uint32_t n = 0;
-    bool invalid = false;
-    if (live) {
-        r.seek(s0);
-        // exactly the codes a one-at-a-time parse reads: every 1-bit code boundary is a code boundary.
-        // The chunk interior first, without bounds (kLeanMargin; by table: lean_step_lut), then the bounded
-        // steps to the chunk end, then the checked steps; a long or invalid code leaves the lean loops
-        // unconsumed.
-        const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
-        // the bounded steps end the parse exactly at the stop -- unless the data ends within reach of the
-        // chunk end (a code running past the limit is invalid: the checked steps)
-        const uint32_t bstop = limit >= stop + 64u ? stop : 0u;
-        Lean c = lean_from(r);
-        bool bad = false;
-        const WinRead rd{win};
-        while (!bad & (c.pos() < fast_stop)) n += lean_step_lut<kSyncLutBits>(rd, s_lut, c, bad);
-        while (!bad & (c.pos() < bstop)) n += lean_step<true>(rd, c, bad, bstop - c.pos());
-        lean_to(r, c);
-        while (r.pos < stop && sync_step(r, stop, limit, n, invalid)) {
-        }
+    const int64_t b = blockIdx.x;
+    const int64_t first = rs ? b * (kEgBlock - 1) - 1 : b * kEgBlock;  // block 0 resolving: chunk -1 (none)
+    stage_columns(P, win, first);
+    __syncthreads();
+    const int64_t ti = first + (int64_t)threadIdx.x;
+    const bool live = ti >= 0 && (uint64_t)ti < P.n_chunks;
+    const uint64_t t = (uint64_t)ti;
+    const int64_t b0 = (int64_t)P.start_bit + ti * (int64_t)kChunkBits;  // absolute bit of the column's bit 0
+    const uint32_t limit = rel_bit(P.limit_bit, b0);
+    const uint32_t stop = min((uint32_t)kChunkBits, limit);
+    const uint32_t* col = column(win);
+    if (DIAG == 1) {
+        if (col[0] == 0x12345678u && P.n_chunks == 0) P.count[0] = 1u;  // keeps the staging
+        return;
     }
-    const uint64_t ex = invalid ? kNoExit : base + r.pos;
+    uint32_t s0 = 0;  // iteration 0 (and chunk 0): the chunk's first bit
+    if (live && iteration > 0 && t > 0) {
+        const uint64_t e = P.exit_in[t - 1];
+        s0 = e == kNoExit ? 0u : rel_bit(e, b0);
+    }
+    uint32_t n = 0, pos = 0;
+    bool invalid = false;
+    if (DIAG == 2) {
+        const uint32_t fast_stop = stop > kLeanMargin ? stop - kLeanMargin : 0u;
+        uint32_t p = 0, w_last = 0;
+        bool bad = false;
+        while (live & !bad & (p < fast_stop)) n += pos_step_lut(col, s_lut, p, bad, w_last);
+        if (n == 0xFFFFFFFFu) P.count[0] = p;
+        return;
+    }
+    if (live) n = parse_chunk(P, col, s_lut, b0, s0, stop, limit, pos, invalid);
+    if (DIAG == 3) {
+        if (n == 0xFFFFFFFFu) P.count[0] = pos;
+        return;
+    }
+    const uint64_t ex = invalid ? kNoExit : (uint64_t)b0 + pos;
     if (!rs) {
         if (!live) return;
         P.exit_out[t] = ex;
@@ -749,64 +909,52 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int it
         if (iteration > 0 && ex != P.exit_in[t]) atomicOr((unsigned int*)&P.status[0], 1u);
         return;
     }
-    s_exit[threadIdx.x] = invalid ? ~0u : r.pos;
+    s_exit[threadIdx.x] = invalid ? ~0u : pos;
     __syncthreads();
-    if (!live || threadIdx.x == 0) return;  // thread 0: the helper chunk (written by its owner block)
-    uint64_t exit = ex;
-    const bool fail = t > 0 && resolve_chunk(win, s_exit[threadIdx.x - 1], s0, r.pos, stop, limit, base, ex, n, exit);
-    P.exit_out[t] = exit;
+    const bool own = live && threadIdx.x > 0;  // thread 0: the helper chunk (written by its owner block)
+    const uint32_t ep = threadIdx.x ? s_exit[threadIdx.x - 1] : ~0u;  // in the chunk before's coordinates
+    // the true start as pass 0 knows it (chunk 0: its first bit)
+    const uint32_t e = t == 0 ? 0u : (ep == ~0u ? ~0u : ep - (uint32_t)kChunkBits);
+    if (DIAG == 4) {
+        if (e == 0x12345678u && n == 0xFFFFFFFFu) P.count[0] = pos;
+        return;
+    }
+    uint32_t x;
+    const bool fail = resolve_block(P, win, s_lut, s_q, s_qn, first, own, e, pos, invalid, stop, limit, b0, n, x);
+    if (DIAG == 5) {
+        if (fail && n == 0xFFFFFFFFu) P.count[0] = x;
+        return;
+    }
+    if (!own) return;
+    P.exit_out[t] = x == ~0u ? kNoExit : (uint64_t)b0 + x;
     P.count[t] = n;
     const uint64_t fb = __ballot(fail);
     if (fb != 0ull && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(fb)) atomicOr((unsigned int*)&P.status[0], 1u);
 }
+__global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
+    sync_body<0>(P, iteration, resolve);
+}
+#ifdef DCT3D_DIAG_FRONT
+__global__ __launch_bounds__(kEgBlock) void eg_sync_diag1_kernel(EgDecParams P) { sync_body<1>(P, 0, 1); }
+__global__ __launch_bounds__(kEgBlock) void eg_sync_diag2_kernel(EgDecParams P) { sync_body<2>(P, 0, 1); }
+__global__ __launch_bounds__(kEgBlock) void eg_sync_diag3_kernel(EgDecParams P) { sync_body<3>(P, 0, 1); }
+__global__ __launch_bounds__(kEgBlock) void eg_sync_diag4_kernel(EgDecParams P) { sync_body<4>(P, 0, 1); }
+__global__ __launch_bounds__(kEgBlock) void eg_sync_diag5_kernel(EgDecParams P) { sync_body<5>(P, 0, 1); }
+#endif
 
-// The chunk's marks are collected in LDS (2 bytes each, relative to the chunk's true start, in the
-// thread's own slot of kMkSlot entries) and written out at the end, each thread its consecutive marks back
-// to back, so that the L2 assembles whole lines: WRITE_SIZE 1.67 GB -> 0.52 GB (the marks' own bytes) and
-// the pass 708 -> 529 us on one box (round 4; stored one at a time as the parse reached them, through a
-// buffer descriptor, each lane's marks tens of microseconds apart, the lines were written back partial).
-// The slots cost 8.5 KiB per block (with the window, 6 blocks per CU instead of 8).  A step's one possible
-// mark is stored branch-free: steps without a mark store to the thread's dummy, 2 bytes behind the
-// window (round 4: an 18th slot entry; an exec-masked store instead compiled to a branch and 13 more VALU
-// per step).
-// Marks leave as the low 16 bits of their bit position (round 5; 64-bit before: 0.52 GB written and read
-// back per c8 step, then 32-bit: 0.27 GB), the whole position of every 64th (a consumer group's first) in
-// mark_base (mark_offset).
-constexpr uint32_t kMkSlot = 17;  // a chunk has at most 17 marks (<= 512 values)
-__global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
-    __shared__ uint32_t win[kSyncWinAlloc];
-    __shared__ uint16_t s_mk[kEgBlock * kMkSlot];
-    __shared__ __attribute__((aligned(16))) uint8_t s_lut[1 << kEgLutBits];
-    copy_lut(s_lut, kEgLut);
-    // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
-    // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
-    // (status[2] != 0) and the host reruns without speculation
-    if (P.status[0] != 0) {  // grid-uniform
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned int*)&P.status[2], 4u);
-        return;
-    }
-    const uint64_t first = (uint64_t)blockIdx.x * kEgBlock;
-    // (the per-chunk loads below issued before the window's staging instead measured 633 -> 745 us)
-    const LdsBits L = stage_block_window(P, win);
-    const uint64_t t = first + threadIdx.x;
-    if (t >= P.n_chunks) return;
-    // the chunk's first value index and true start: both loads in flight together, at the top issue
-    // priority (one round trip, not two behind the other blocks' parse work)
-    __builtin_amdgcn_s_setprio(3);
-    const uint64_t idx0 = P.off[t];
-    // the converged exits are in exit_in (the host swaps the buffers after every pass)
-    const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];
-    __builtin_amdgcn_s_setprio(0);
-    if (idx0 >= P.n_values) return;
-    if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
-    const uint64_t base = L.w0 * 32;
-    const uint32_t end = rel_bit(P.start_bit + (t + 1) * kChunkBits, base);
-    const uint32_t limit = rel_bit(P.limit_bit, base);
-    WinReader r{win, kSyncWinWords, 0, 0, 0, 0, 0};
-    const uint32_t sp = rel_bit(s, base);  // the chunk's true start (LDSM marks are relative to it)
-    r.seek(sp);
-    uint16_t* const myk = s_mk + threadIdx.x * kMkSlot;  // mark k of the chunk (value 32 k - ph) at myk[k]
-    uint16_t* const dummy = (uint16_t*)(win + kSyncWinWords) + threadIdx.x;  // a step without a mark stores here
+// The mark parse of one chunk from its true start sp (chunk-relative) with its first value idx0: the bit
+// position of every 32nd value.  The marks are collected in the thread's slot myk (2 bytes each, relative
+// to the true start; kMkSlot entries, the last a dummy target for steps without a mark: no branch) and
+// written out at the end, each thread its consecutive marks back to back, so that the L2 assembles whole
+// lines (round 4: WRITE_SIZE 1.67 -> 0.52 GB, the pass 708 -> 529 us; stored one at a time as the parse
+// reached them the lines were written back partial).  Marks leave as the low 16 bits of their bit position
+// (round 5), the whole position of every 64th (a consumer group's first) in mark_base (mark_offset).
+constexpr uint32_t kMkSlot = 17;  // 16 marks (a chunk's true parse takes <= 512 values) + the dummy
+template <bool WRITE = true>
+__device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t* col, const uint8_t* lut, uint16_t* myk,
+                                           int64_t b0, uint32_t sp, uint64_t idx0) {
+    const uint32_t end = (uint32_t)kChunkBits;
+    const uint32_t limit = rel_bit(P.limit_bit, b0);
     // chunk-relative 32-bit value count i (value idx0 + i): the 64-bit index arithmetic per step was a
     // large part of the pass.  A chunk holds at most ~kChunkBits + 64 codes, so rem below never binds
     // unless the wanted values end inside this chunk.
@@ -814,88 +962,275 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) {
     const uint32_t rem = (uint32_t)min(rem64, (uint64_t)(2 * kChunkBits));
     const bool ends_here = rem64 <= 2 * kChunkBits;
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
+    const uint32_t sh = ph ? 1u : 0u;       // slot of value j: (ph + j) / 32 - sh (16 slots)
     const uint64_t gm0 = idx0 / kMarkVals;  // mark gm0 + k = mark of value idx0 + 32 k - ph
+    uint16_t* const dummy = myk + (kMkSlot - 1);
     uint32_t i = 0, code;
     // Interior of the chunk: a step moves at most 31 + 31 bits and 32 values, so while the parse is
     // kLeanMargin bits short of the chunk end and of the data limit none of the bounds below can bind -- a
     // lean loop without them (a long or invalid code leaves it for the checked loop, which reads or reports
     // it).  The lean loops run only in chunks that cannot hold the last wanted value (rem64 > 2 kChunkBits;
     // the few others take the checked steps whole): there the value count never binds, and the loops test
-    // only the position (round 5: 53 -> 50 VALU per step with the running mark index and slot below).
+    // only the position.
     const uint32_t lim_end = ends_here ? 0u : min(end, limit);
     const uint32_t fast_end = lim_end > kLeanMargin ? lim_end - kLeanMargin : 0u;
+    uint32_t p = sp;
     {
-        Lean c = lean_from(r);
         bool bad = false;
-        const WinRead rd{win};
         // the next mark: chunk-relative value index nm (value idx0 + nm), its slot mp; a step takes nv <= 32
         // values, so at most one mark, value d0 = nm - i of the step
         uint32_t nm = (0u - ph) & (kMarkVals - 1);
-        uint16_t* mp = myk + (ph + nm) / kMarkVals;
-        const uint32_t s0 = 0u - sp;  // (bit positions leave relative to the chunk's true start)
+        uint16_t* mp = myk;
         auto mark = [&](uint32_t at, uint32_t nv, uint32_t d0) {
             const bool hit = d0 < nv;
-            *(hit ? mp : dummy) = (uint16_t)(at + s0);  // no branch
+            *(hit ? mp : dummy) = (uint16_t)(at - sp);  // no branch
             nm += hit ? kMarkVals : 0u;
             mp += hit ? 1 : 0;
             i += nv;
         };
         // table steps that stop on the mark (nv <= 32): the mark is value d0 of the step, at bit p0 + d0
-        while (!bad & (c.pos() < fast_end)) {
-            const uint32_t p0 = c.pos();
+        uint32_t w_last = 0;
+        while (!bad & (p < fast_end)) {
+            const uint32_t p0 = p;
             const uint32_t d0 = nm - i;
-            mark(p0 + d0, lean_step_lut_mark(rd, s_lut, c, bad, d0), d0);
+            mark(p0 + d0, pos_step_lut_mark(col, lut, p, bad, d0, w_last), d0);
         }
+        // the long or invalid code the last step met (its mark, if it is one, was stored at its first bit:
+        // the checked loop stores the same or ends the pass)
+        pos_step_undo(bad, w_last, p, i);
         // to the chunk end exactly (as the sync pass; the chunk holding the last wanted value and the data's
         // end take the checked steps)
         const uint32_t bend = limit >= end + 64u && !ends_here ? end : 0u;
-        while (!bad & (c.pos() < bend)) {
-            const uint32_t p0 = c.pos();
+        while (!bad & (p < bend)) {
+            const uint32_t p0 = p;
             const uint32_t d0 = nm - i;
-            mark(p0 + d0, lean_step<true>(rd, c, bad, bend - p0), d0);
+            mark(p0 + d0, pos_step_lut_mark_bounded(col, lut, p, bad, d0, bend), d0);
         }
-        lean_to(r, c);
     }
-    while (i < rem && r.pos < end) {
-        const uint32_t p0 = r.pos;
-        if (p0 >= limit) {  // ran out of bits
-            atomicOr((unsigned int*)&P.status[2], 2u);
-            return;
+    if (i < rem && p < end) {
+        ColReader r{col, &P, (uint64_t)b0, 0, 0, 0, 0, 0};
+        r.seek(p);
+        while (i < rem && r.pos < end) {
+            const uint32_t p0 = r.pos;
+            if (p0 >= limit) {  // ran out of bits
+                atomicOr((unsigned int*)&P.status[2], 2u);
+                return;
+            }
+            // one step = a run of 1-bit codes, then one longer code (as sync_step)
+            const uint32_t room = min(min(end - p0, limit - p0), rem - i);
+            const uint32_t k = r.ones(min(room, 64u));
+            if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
+                for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
+                    myk[(ph + j) / kMarkVals - sh] = (uint16_t)(p0 + (j - i) - sp);
+                i += k;
+                if (ends_here && i == rem) P.status[1] = (uint64_t)b0 + r.pos;  // the bit after the last wanted value
+            }
+            // the run ended the chunk or the wanted values, or the buffered bits ran out inside it (refill)
+            if (i >= rem || r.pos >= end || !r.at_long_code()) continue;
+            const uint32_t p1 = r.pos;
+            if (!r.get(code) || r.pos > limit) {
+                // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
+                atomicOr((unsigned int*)&P.status[2], (uint64_t)p1 + 32 <= limit && r.pos <= limit ? 1u : 2u);
+                return;
+            }
+            // a code of 33+ bits (|v| >= 2^15): the consumers' parse steps check for them (parse_step CHECK).
+            // Every code of the wanted values is parsed here or in the lean loops above, which leave every
+            // such code to this loop.
+            if (code >= 0x10000u) atomicOr((unsigned int*)&P.status[3], 1u);
+            if (((ph + i) & (kMarkVals - 1)) == 0) myk[(ph + i) / kMarkVals - sh] = (uint16_t)(p1 - sp);
+            if (++i == rem && ends_here) P.status[1] = (uint64_t)b0 + r.pos;
         }
-        // one step = a run of 1-bit codes, then one longer code (as sync_step): every lane advances
-        // through both halves each iteration, instead of the wave running a run-only and a code-only
-        // iteration for lanes that are in different halves
-        const uint32_t room = min(min(end - p0, limit - p0), rem - i);
-        const uint32_t k = r.ones(min(room, 64u));
-        if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
-            for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
-                myk[(ph + j) / kMarkVals] = (uint16_t)(p0 + (j - i) - sp);
-            i += k;
-            if (ends_here && i == rem) P.status[1] = base + r.pos;  // the bit after the last wanted value
-        }
-        // the run ended the chunk or the wanted values, or the buffered bits ran out inside it (refill)
-        if (i >= rem || r.pos >= end || !r.at_long_code()) continue;
-        const uint32_t p1 = r.pos;
-        if (!r.get(code) || r.pos > limit) {
-            // ran out of bits (2) unless 32 zero bits lie inside the data (corrupt, 1)
-            atomicOr((unsigned int*)&P.status[2], (uint64_t)p1 + 32 <= limit && r.pos <= limit ? 1u : 2u);
-            return;
-        }
-        // a code of 33+ bits (|v| >= 2^15): the consumers' parse steps check for them (parse_step CHECK).
-        // Every code of the wanted values is parsed here or in the lean loops above, which leave every
-        // such code to this loop.
-        if (code >= 0x10000u) atomicOr((unsigned int*)&P.status[3], 1u);
-        if (((ph + i) & (kMarkVals - 1)) == 0) myk[(ph + i) / kMarkVals] = (uint16_t)(p1 - sp);
-        if (++i == rem && ends_here) P.status[1] = base + r.pos;
     }
-    // the chunk's marks k = (ph ? 1 : 0) .. (ph + i - 1) / 32, back to back
-    const uint64_t b0 = base + sp;
+    if (!WRITE) {  // diagnostic
+        if (i == 0xFFFFFFFFu) P.mark[0] = (uint16_t)p;
+        return;
+    }
+    // the chunk's marks k = sh .. (ph + i - 1) / 32, back to back
+    const uint64_t a0 = (uint64_t)b0 + sp;
     uint16_t* const mk = P.mark + gm0;
-    for (uint32_t k = ph ? 1u : 0u; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) {
-        const uint64_t m = b0 + myk[k];
+    for (uint32_t k = sh; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) {
+        const uint64_t m = a0 + myk[k - sh];
         mk[k] = (uint16_t)m;
         if (((gm0 + k) & (kMarkGroup - 1)) == 0) P.mark_base[(gm0 + k) / kMarkGroup] = m;
     }
+}
+
+// Mark pass (the non-speculative path): each chunk parsed once more from its true start (the converged
+// exit of the chunk before), its first value index from the scan.
+template <int DIAG>
+__device__ __forceinline__ void mark_body(const EgDecParams& P) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock * kMkSlot / 2 + 1];
+    uint8_t* const s_lut = (uint8_t*)lds;
+    uint32_t* const win = lds + kLutBytes / 4;
+    uint16_t* const s_mk = (uint16_t*)(win + kColBytes / 4);
+    copy_lut(s_lut);
+    // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
+    // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
+    if (P.status[0] != 0) {  // grid-uniform
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr((unsigned int*)&P.status[2], 4u);
+        return;
+    }
+    const int64_t first = (int64_t)blockIdx.x * kEgBlock;
+    stage_columns(P, win, first);
+    __syncthreads();
+    if (DIAG == 1) {
+        if (column(win)[0] == 0x12345678u && P.n_chunks == 0) P.count[0] = 1u;  // keeps the staging
+        return;
+    }
+    const uint64_t t = (uint64_t)first + threadIdx.x;
+    if (t >= P.n_chunks) return;
+    // the chunk's first value index and true start: both loads in flight together, at the top issue
+    // priority (one round trip, not two behind the other blocks' parse work)
+    __builtin_amdgcn_s_setprio(3);
+    const uint64_t idx0 = P.off[t];
+    const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];  // the converged exits
+    __builtin_amdgcn_s_setprio(0);
+    if (idx0 >= P.n_values) return;
+    if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
+    const int64_t b0 = (int64_t)P.start_bit + (int64_t)t * (int64_t)kChunkBits;
+    mark_chunk<DIAG == 0>(P, column(win), s_lut, s_mk + threadIdx.x * kMkSlot, b0, rel_bit(s, b0), idx0);
+}
+__global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) { mark_body<0>(P); }
+#ifdef DCT3D_DIAG_FRONT
+__global__ __launch_bounds__(kEgBlock) void eg_mark_diag1_kernel(EgDecParams P) { mark_body<1>(P); }
+__global__ __launch_bounds__(kEgBlock) void eg_mark_diag2_kernel(EgDecParams P) { mark_body<2>(P); }
+#endif
+
+// The fused front (round 6): the resolving sync pass, the scan of the chunk counts and the mark pass in
+// one launch, the stream staged into LDS once.  Block b: pass 0 and the resolve walk of its 255 chunks (as
+// eg_sync_kernel), a block scan of their true counts, then the counts of every earlier block by a
+// decoupled look-back over per-block descriptors (desc[b]: flag in the top 2 bits -- 1 aggregate, 2
+// inclusive prefix, 3 failed -- the value below; zeroed by the host before the launch), then the mark
+// parse of each chunk from its true start (the pass-0 exit of the chunk before, in LDS).  Forward progress:
+// a block only waits for lower-numbered blocks, which the dispatcher started before it; a wait longer than
+// kFrontSpin sleeps (never seen) gives up as failed.  A failed block (a chunk that did not resolve, or the
+// wait) makes every later block fail too: no marks there, status[0] and status[2] bit 4 set, the consumer
+// skips itself and the host reruns the non-speculative front (eg_sync_kernel passes, scan, eg_mark_kernel).
+// Replaces: sync pass 0 (its window staging), the three scan launches, the mark pass's window staging and
+// its reads of the chunk offsets and exits.
+constexpr uint64_t kDescAgg = 1ull << 62, kDescInc = 2ull << 62, kDescFail = 3ull << 62;
+constexpr uint64_t kDescVal = (1ull << 62) - 1;
+constexpr uint32_t kFrontSpin = 1u << 16;
+__global__ __launch_bounds__(kEgBlock) void eg_front_kernel(EgDecParams P, uint64_t* desc, int force_fail) {
+    __shared__ __attribute__((aligned(16)))
+    uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock + kEgBlock * kMkSlot / 2 + kEgWaves + 6];
+    static_assert(kEgBlock * kMkSlot / 2 >= 2 * kEgBlock, "the walk queue fits the mark slots");
+    uint8_t* const s_lut = (uint8_t*)lds;
+    uint32_t* const win = lds + kLutBytes / 4;
+    uint32_t* const s_exit = win + kColBytes / 4;
+    uint16_t* const s_mk = (uint16_t*)(s_exit + kEgBlock);
+    uint32_t* const s_wsum = s_exit + kEgBlock + kEgBlock * kMkSlot / 2;  // per-wave count sums
+    uint64_t* const s_misc = (uint64_t*)(s_wsum + kEgWaves);             // [0] prefix, [1] failed
+    uint32_t* const s_qn = (uint32_t*)(s_misc + 2);
+    uint32_t* const s_q = (uint32_t*)s_mk;  // the resolve's walk queue, before the mark slots are used
+    copy_lut(s_lut);
+    if (threadIdx.x == 0) *s_qn = 0u;
+    const int64_t b = blockIdx.x;
+    const int64_t first = b * (kEgBlock - 1) - 1;
+    stage_columns(P, win, first);
+    __syncthreads();
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t ti = first + (int64_t)tid;
+    const bool live = ti >= 0 && (uint64_t)ti < P.n_chunks;
+    const uint64_t t = (uint64_t)ti;
+    const int64_t b0 = (int64_t)P.start_bit + ti * (int64_t)kChunkBits;
+    const uint32_t limit = rel_bit(P.limit_bit, b0);
+    const uint32_t stop = min((uint32_t)kChunkBits, limit);
+    const uint32_t* col = column(win);
+    // pass 0 from the chunk's first bit
+    uint32_t n = 0, pos = 0;
+    bool invalid = false;
+    if (live) n = parse_chunk(P, col, s_lut, b0, 0u, stop, limit, pos, invalid);
+    s_exit[tid] = invalid ? ~0u : pos;
+    __syncthreads();
+    // the resolve: the true count and the true start (the pass-0 exit of the chunk before, which the walk
+    // proves true unless it fails) of each owned chunk (threads 1 .. 255)
+    const bool own = live && tid > 0;
+    const uint32_t ep = tid ? s_exit[tid - 1] : ~0u;
+    const uint32_t sp = t == 0 ? 0u : (ep == ~0u ? ~0u : ep - (uint32_t)kChunkBits);
+    uint32_t cnt = n, x;
+    const bool fail = resolve_block(P, win, s_lut, s_q, s_qn, first, own, sp, pos, invalid, stop, limit, b0, cnt, x);
+    if (!own) cnt = 0;
+    // block scan of the counts (the helper's is 0): in the wave by shuffles, across the 4 waves in LDS
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    const bool wfail = __ballot(fail) != 0ull;
+    if (tid == 0) s_misc[1] = 0;
+    __syncthreads();
+    if ((wfail || force_fail) && lane == 0) atomicOr((unsigned int*)&s_misc[1], 1u);
+    uint64_t wpre = 0, agg = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kEgWaves; w++) {
+        wpre += w < wave ? s_wsum[w] : 0u;
+        agg += s_wsum[w];
+    }
+    __syncthreads();
+    // the look-back (wave 0): the counts of every chunk before the block's first
+    if (wave == 0) {
+        bool failed = s_misc[1] != 0;
+        uint64_t excl = 0;
+#ifdef DCT3D_FRONT_NO_LOOKBACK  // diagnostic build (timing only): the prefix from a scan run before the front
+        excl = (uint64_t)b * (kEgBlock - 1) < P.n_chunks ? P.off[b * (kEgBlock - 1)] : 0;
+        if (false) {
+#else
+        if (b > 0) {
+#endif
+            if (lane == 0)
+                __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescAgg | agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t look = b - 1;
+            uint32_t spins = 0;
+            while (!failed) {
+                const int64_t i = look - (int64_t)lane;
+                const uint64_t d = i >= 0 ? __hip_atomic_load(&desc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : kDescInc;  // before block 0: an inclusive prefix of 0
+                const uint32_t flag = (uint32_t)(d >> 62);
+                const uint64_t stopm = __ballot(flag >= 2u);  // an inclusive prefix or a failure
+                const uint32_t s = stopm ? (uint32_t)__builtin_ctzll(stopm) : 64u;
+                const uint64_t upto = s >= 63u ? ~0ull : (2ull << s) - 1ull;  // lanes 0 .. s
+                if ((__ballot(flag == 0u) & upto) != 0ull) {  // a predecessor not published yet: wait
+                    if (++spins > kFrontSpin) failed = true;
+                    __builtin_amdgcn_s_sleep(4);
+                    continue;
+                }
+                if (s < 64u && __shfl(flag, s, 64) == 3u) {
+                    failed = true;
+                    break;
+                }
+                uint64_t v = lane <= s ? (d & kDescVal) : 0ull;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+                excl += v;
+                if (s < 64u) break;
+                look -= 64;
+            }
+        }
+        if (lane == 0) {
+            __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescInc | (excl + agg)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            s_misc[0] = excl;
+            s_misc[1] = failed ? 1u : 0u;
+            // the total count (the scan's, status[4]: fewer values than wanted is ENODATA)
+            if (!failed && b == (int64_t)gridDim.x - 1) P.status[4] = excl + agg;
+
+        }
+    }
+    __syncthreads();
+    if (s_misc[1] != 0) {  // block-uniform: rerun without speculation
+        if (tid == 0) {
+            atomicOr((unsigned int*)&P.status[0], 1u);
+            atomicOr((unsigned int*)&P.status[2], 4u);
+        }
+        return;
+    }
+    if (!own || sp == ~0u) return;  // sp = ~0u: the true parse stopped in an earlier chunk (reported there)
+    const uint64_t idx0 = s_misc[0] + wpre + (incl - cnt);
+    if (idx0 >= P.n_values) return;
+    mark_chunk(P, col, s_lut, s_mk + tid * kMkSlot, b0, sp, idx0);
 }
 
 template <int D>
@@ -994,6 +1329,16 @@ int launch_eg_sync(const EgDecParams& P, int iteration, int resolve, hipStream_t
     if (P.n_chunks == 0) return 0;
     const bool rs = iteration == 0 && resolve;
     const uint64_t per = rs ? kEgBlock - 1 : kEgBlock;
+#ifdef DCT3D_DIAG_FRONT  // diagnostic build: the resolving pass's parts before it (timing only)
+    if (rs) {
+        const dim3 g((uint32_t)((P.n_chunks + per - 1) / per));
+        hipLaunchKernelGGL(eg_sync_diag1_kernel, g, dim3(kEgBlock), 0, st, P);
+        hipLaunchKernelGGL(eg_sync_diag2_kernel, g, dim3(kEgBlock), 0, st, P);
+        hipLaunchKernelGGL(eg_sync_diag3_kernel, g, dim3(kEgBlock), 0, st, P);
+        hipLaunchKernelGGL(eg_sync_diag4_kernel, g, dim3(kEgBlock), 0, st, P);
+        hipLaunchKernelGGL(eg_sync_diag5_kernel, g, dim3(kEgBlock), 0, st, P);
+    }
+#endif
     hipLaunchKernelGGL(eg_sync_kernel, dim3((uint32_t)((P.n_chunks + per - 1) / per)), dim3(kEgBlock), 0, st, P,
                        iteration, (int)rs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1024,8 +1369,22 @@ int launch_eg_stitch(const EgParams& P, hipStream_t st) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// desc: one zeroed word per block (front_blocks); force_fail (test option): every block fails
+uint64_t front_blocks(uint64_t n_chunks) { return (n_chunks + kEgBlock - 2) / (kEgBlock - 1); }
+int launch_eg_front(const EgDecParams& P, uint64_t* desc, int force_fail, hipStream_t st) {
+    if (P.n_chunks == 0) return 0;
+    const uint64_t blocks = front_blocks(P.n_chunks);
+    if (blocks > 0x7FFFFFFFull) return -1;
+    hipLaunchKernelGGL(eg_front_kernel, dim3((uint32_t)blocks), dim3(kEgBlock), 0, st, P, desc, force_fail);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_eg_mark(const EgDecParams& P, hipStream_t st) {
     if (P.n_chunks == 0) return 0;
+#ifdef DCT3D_DIAG_FRONT  // diagnostic build: the mark pass's parts before it (timing only)
+    hipLaunchKernelGGL(eg_mark_diag1_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+    hipLaunchKernelGGL(eg_mark_diag2_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
+#endif
     hipLaunchKernelGGL(eg_mark_kernel, dim3((uint32_t)((P.n_chunks + kEgBlock - 1) / kEgBlock)), dim3(kEgBlock), 0, st, P);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -794,10 +794,21 @@ __device__ __forceinline__ void e16_recheck64(const uint2 (&raw)[4], double bv, 
 // (72 VGPRs) is what the main path needs; the attribute keeps the rare paths from raising it (the
 // kernel needs no scratch: tools/isa_count.py).
 static_assert(kMaxGroupsDev * (4 + 8) <= kE16Lds, "exact-replay scratch fits the wave's region");
+// Diagnostic traversal (MODES 4 / 5): wave slot s, counted strip-major (stack, strip, block row, column in
+// the strip), -> the cube it encodes (the reference's cube-major index, so the output is unchanged)
+__device__ __forceinline__ uint32_t strip_cube(const EncodeParams& P, uint32_t s) {
+    const uint32_t st = fdiv(s, P.div_cps);
+    const uint32_t r = s - st * P.cubes_per_stack;
+    const uint32_t strip = fdiv(r, P.div_strip_cubes);
+    const uint32_t rr = r - strip * P.strip_cubes;
+    const uint32_t by = fdiv(rr, P.div_strip_w);
+    return st * P.cubes_per_stack + by * P.nbx + strip * P.strip_w + (rr - by * P.strip_w);
+}
 template <bool NT, int MODE = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void encode16_kernel(EncodeParams P) {
     constexpr int CS = 512;
-    constexpr bool MEM = MODE == 1, COMP = MODE == 2, TRACE = MODE == 3;
+    // MODE 4 / 5: MODE 1 / 0 with the strip traversal (diagnostic sweep)
+    constexpr bool MEM = MODE == 1 || MODE == 4, COMP = MODE == 2, TRACE = MODE == 3, STRIP = MODE >= 4;
     uint64_t t_start = 0, t_comp = 0;
     if constexpr (TRACE) t_start = __builtin_amdgcn_s_memrealtime();
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * kE16Lds];
@@ -807,7 +818,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
 #ifndef DCT3D_E16_XCD_G  // A/B only: the XCD tile run length of encode16_kernel
 #define DCT3D_E16_XCD_G 64
 #endif
-    const uint32_t cube0 = P.g_base + (xcd_tile<DCT3D_E16_XCD_G>() * kWavesPerBlock + wave) * kE16CPW;
+    const uint32_t slot0 = P.g_base + (xcd_tile<DCT3D_E16_XCD_G>() * kWavesPerBlock + wave) * kE16CPW;
+    uint32_t cube0 = slot0;
+    if constexpr (STRIP) cube0 = slot0 < P.n_cubes ? strip_cube(P, slot0) : slot0;
     const int k = lane & 7, h = (lane >> 4) & 1;
     const int c = (lane >> 5) * 2 + ((lane & 15) >> 3);
     const uint32_t g = cube0 + c;

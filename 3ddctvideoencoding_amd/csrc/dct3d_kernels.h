@@ -46,6 +46,10 @@ struct EncodeParams {
     const double* tab64;       // 8x8x8 second certificate: [64] fp64 basis [k][n], [32] thresholds per s
     uint32_t recheck;          // 1: run the second certificate (0: test option, all open -> Java fold)
     uint64_t* trace;           // MODE 3 (diagnostic timeline): per wave {start, transform done, stored, hw id}
+    // MODES 4 / 5 (diagnostic traversal sweep): the waves walk the cubes in vertical strips of strip_w
+    // cubes (strip_cubes = strip_w * block rows per stack), row-major within a strip (strip_cube)
+    uint32_t strip_w, strip_cubes;
+    FastDiv div_strip_w, div_strip_cubes;
 };
 
 struct DecodeParams {
@@ -172,6 +176,10 @@ int launch_eg_sync(const EgDecParams& P, int iteration, int resolve, hipStream_t
 int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
 int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mark pass + emit
 int launch_eg_mark(const EgDecParams& P, hipStream_t st);
+// the fused front (resolving sync pass + scan + mark pass in one launch; desc: front_blocks(n_chunks) zeroed
+// words); a chunk that does not resolve: status[2] bit 4 (rerun without speculation)
+uint64_t front_blocks(uint64_t n_chunks);
+int launch_eg_front(const EgDecParams& P, uint64_t* desc, int force_fail, hipStream_t st);
 int launch_eg_emit(int D, const EgDecParams& P, hipStream_t st);
 // fused stream -> raster decode: values parsed at the marks straight into the decode's LDS staging
 // groups_per_wave: 1, 2, 4 or 8 (other values: 8) groups of CPW cubes per wave, the next one's loads ahead

@@ -71,6 +71,7 @@ struct dct3d_ctx {
     bool opt_enc_no_recheck = false, opt_eg_two_step = false,
          opt_eg_no_resolve = false;
     bool opt_eg_force_retry = false;
+    bool opt_eg_fused_front = false;
     int opt_eg_dec_groups = 0;  // fused stream decode: groups per wave (0: the default, 8)
     // certify-or-replay state
     uint64_t last_units = 0;
@@ -94,7 +95,7 @@ struct dct3d_ctx {
     DevBuf d_egf_slot;
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     // (d_egd_status: the decode's four status words, then the scan's two -- one read-back per call)
-    DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark;
+    DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark, d_egd_desc;
     // pinned host words the entropy stages' status lands in (one DMA read-back, not a pageable copy)
     uint64_t* h_status = nullptr;
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
@@ -267,7 +268,7 @@ void dct3d_ctx_destroy(dct3d_ctx* c) {
     for (DevBuf* b : {&c->d_ngroups, &c->d_coef, &c->d_group_of, &c->d_inv_coef, &c->d_tabs, &c->d_tabs64,
                       &c->d_enc_counts, &c->h_in, &c->h_out, &c->h_aux, &c->d_diag, &c->d_eg_bits,
                       &c->d_eg_off, &c->d_eg_bsum, &c->d_eg_status, &c->d_eg_out, &c->d_eg_q, &c->d_eg_ht,
-                      &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egd_mark,
+                      &c->d_egd_exit, &c->d_egd_status, &c->d_egd_in, &c->d_egd_raster, &c->d_egd_mark, &c->d_egd_desc,
                       &c->d_egf_slot})
         b->release();
     if (c->h_status) (void)hipHostFree(c->h_status);
@@ -324,6 +325,7 @@ int dct3d_ctx_set_option(dct3d_ctx* c, int option, double value) {
         case DCT3D_OPT_EG_TWO_STEP: c->opt_eg_two_step = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_NO_RESOLVE: c->opt_eg_no_resolve = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_FORCE_RETRY: c->opt_eg_force_retry = value != 0.0; return DCT3D_OK;
+        case DCT3D_OPT_EG_FUSED_FRONT: c->opt_eg_fused_front = value != 0.0; return DCT3D_OK;
         case DCT3D_OPT_EG_DEC_GROUPS:
             if (value != 0.0 && value != 1.0 && value != 2.0 && value != 4.0 && value != 8.0) return DCT3D_EINVAL;
             c->opt_eg_dec_groups = (int)value;
@@ -997,6 +999,20 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.mark_base = (uint64_t*)c->d_egd_mark.p;
     D.mark = (uint16_t*)(D.mark_base + n_mark_groups);
     D.q = nullptr;
+#ifdef DCT3D_FRONT_NO_LOOKBACK
+    if (false) {
+#else
+    if (spec && c->opt_eg_fused_front) {
+#endif
+        // A/B option: the fused front, one launch (eg_front_kernel); the consumer reads its verdict on the device
+        const uint64_t nb = front_blocks(n_chunks);
+        if ((rc = c->d_egd_desc.grow(nb * sizeof(uint64_t)))) return rc;
+        if (hipMemsetAsync(c->d_egd_status.p, 0, kEgdStatusBytes, c->stream) != hipSuccess ||
+            hipMemsetAsync(c->d_egd_desc.p, 0, nb * sizeof(uint64_t), c->stream) != hipSuccess)
+            return DCT3D_EDEVICE;
+        if (launch_eg_front(D, (uint64_t*)c->d_egd_desc.p, c->opt_eg_force_retry ? 1 : 0, c->stream)) return DCT3D_EKERNEL;
+        return DCT3D_OK;
+    }
     // sync passes until no chunk exit changes (pass 0 parses from the nominal chunk starts and, resolving,
     // usually proves every chunk in sync by itself; otherwise confirming passes follow); at most
     // n_chunks + 1 passes by induction from chunk 0.  DCT3D_OPT_EG_NO_RESOLVE: always confirm (A/B, tests)
@@ -1009,8 +1025,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
         if (launch_eg_sync(D, (int)(it < 2 ? it : 1), resolve, c->stream)) return DCT3D_EKERNEL;
         cur ^= 1;
         if (it == 0 && !resolve) continue;
-        if (it == 0 && spec) {  // the verdict is read on the device (eg_mark_kernel)
-            // test option: a failed verdict, to exercise the skip-and-rerun path
+        if (it == 0 && spec) {  // speculative front: the verdict is read on the device (eg_mark_kernel)
             if (c->opt_eg_force_retry && hipMemsetAsync(c->d_egd_status.p, 0x01, 1, c->stream) != hipSuccess)
                 return DCT3D_EDEVICE;
             break;
@@ -1031,6 +1046,14 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     S.out_cap_words = ~0ull;
     if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
+#ifdef DCT3D_FRONT_NO_LOOKBACK  // diagnostic build: the fused front after the scan, its prefixes from it
+    if (spec) {
+        const uint64_t nb = front_blocks(n_chunks);
+        if ((rc = c->d_egd_desc.grow(nb * sizeof(uint64_t)))) return rc;
+        if (launch_eg_front(D, (uint64_t*)c->d_egd_desc.p, 0, c->stream)) return DCT3D_EKERNEL;
+        return DCT3D_OK;
+    }
+#endif
     if (launch_eg_mark(D, c->stream)) return DCT3D_EKERNEL;
     return DCT3D_OK;
 }

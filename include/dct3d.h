@@ -136,6 +136,10 @@ int dct3d_ctx_info(const dct3d_ctx *ctx, int *device, int *block_d, void **hip_s
                                          pass 0, so the call takes its skip-and-rerun path (same results) */
 #define DCT3D_OPT_EG_DEC_GROUPS 9     /* stream -> raster decode: groups of 2,048 values per wave, the next
                                          group's loads in flight during the current one (1, 2, 4, 8; 0: 8) */
+#define DCT3D_OPT_EG_FUSED_FRONT 10   /* 1: the Exp-Golomb decode's speculative front as ONE launch (the
+                                         resolving sync pass, the chunk scan and the mark pass fused, a
+                                         decoupled look-back for the chunks' value indices) instead of three
+                                         (A/B: measured slower) */
 int dct3d_ctx_set_option(dct3d_ctx *ctx, int option, double value);
 /* Enable HIP-event timing of the kernels (reported by dct3d_get_stats). */
 int dct3d_ctx_set_profiling(dct3d_ctx *ctx, int on);

@@ -43,6 +43,14 @@ int dct3d_encode_diag_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, in
 int dct3d_encode_trace_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                            int32_t *d_q, int mode, uint64_t *d_trace);
 
+/* Traversal sweep (the 4K shard's read pattern): the 8x8x8 encode with its waves walking the
+ * cubes in vertical strips of strip_w cubes (strip-major: stack, strip, block row, column in the strip)
+ * instead of the product's row-major order; the output is the same cube-major array.  mode 1 = memory
+ * only (as dct3d_encode_diag_dev mode 1; d_q is NOT a DCT), mode 0 = the full encode (d_q IS the encode,
+ * rare paths included, no replay counters).  strip_w: a multiple of 4 dividing width / 8. */
+int dct3d_encode_strip_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
+                           int32_t *d_q, int mode, int strip_w);
+
 /* The decode kernel split in two (bench support; d_raster receives NOT a decode): mode 1 = memory only
  * (the same staged loads and raster stores, no transform), mode 2 = compute only (no global loads, no
  * stores).  The decode's time read against both shows how far its memory and its fp64 issue overlap

@@ -322,18 +322,20 @@ def _eg_decode_q(ctx, data: bytes, n_cubes: int):
     return dq.cpu().numpy().reshape(n_cubes, ctx.bd, 8, 8), eb
 
 
-def test_speculative_front_rerun_on_unresolved_pass0(pkg, oracle, plan8, gpu_ctx8):
-    """The stream decode enqueues its scan, mark pass and consumer right behind the resolving sync pass
-    (no host round trip); should pass 0 not resolve, the mark pass writes nothing, the consumer skips
-    itself and the call reruns without speculation.  DCT3D_OPT_EG_FORCE_RETRY forces that verdict: the
-    three entry points (two-step, fused device, fused host) give the same results and errors."""
+@pytest.mark.parametrize("fused", [0, 1])
+def test_speculative_front_rerun_on_unresolved_pass0(pkg, oracle, plan8, gpu_ctx8, fused):
+    """The stream decode enqueues its front (the resolving sync pass, the scan and the mark pass; or, as
+    an option, the fused eg_front_kernel) and the consumer without a host round trip; should pass 0 not resolve, no
+    marks are written, the consumer skips itself and the call reruns without speculation.
+    DCT3D_OPT_EG_FORCE_RETRY forces that verdict: the three entry points (two-step, fused device, fused
+    host) give the same results and errors."""
     fr = pkg.synthetic.frames(128, 64, 24, kind="uniform", frame0=4)
     q = plan8.encode_q(fr)
     data, nbits = _expected(oracle, pkg, q, 8)
     ref_fused, eb0 = _decode_fused(gpu_ctx8, data, 128, 64, 3)
     ref_two, eb1 = _decode_two_step(gpu_ctx8, data, 128, 64, 3)
     ref_host, eb2 = gpu_ctx8.decode_eg(data, 128, 64, 3)
-    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_FORCE_RETRY, 1):
+    with ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_FORCE_RETRY, 1), ctx_option(gpu_ctx8, pkg.DCT3D_OPT_EG_FUSED_FRONT, fused):
         got_fused, e0 = _decode_fused(gpu_ctx8, data, 128, 64, 3)
         got_two, e1 = _decode_two_step(gpu_ctx8, data, 128, 64, 3)
         got_host, e2 = gpu_ctx8.decode_eg(data, 128, 64, 3)
@@ -390,3 +392,21 @@ def test_fused_decode_tiny_frames(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4,
     n = ctx.n_cubes(w, h, 1)
     qd, eb2 = _eg_decode_q(ctx, data, n)
     assert eb2 == nbits and np.array_equal(qd, q.reshape(n, depth, 8, 8))
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("kind", ["ramp", "uniform"])
+def test_fused_front_option_same_results(pkg, gpu_ctx8, gpu_ctx4, depth, kind):
+    """DCT3D_OPT_EG_FUSED_FRONT: the one-launch front (eg_front_kernel: resolve, block scan, decoupled
+    look-back, marks) gives the three-launch front's raster and end bit at 1080p (~22 k look-back blocks
+    per call), through both consumers."""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = pkg.synthetic.frames(1920, 1080, 2 * depth, kind=kind, frame0=7)
+    data, tb = ctx.encode_eg(fr)
+    ref, reb = _decode_fused(ctx, data, 1920, 1080, 2)
+    qref, qeb = _eg_decode_q(ctx, data, ctx.n_cubes(1920, 1080, 2))
+    with ctx_option(ctx, pkg.DCT3D_OPT_EG_FUSED_FRONT, 1):
+        got, eb = _decode_fused(ctx, data, 1920, 1080, 2)
+        qgot, qeb2 = _eg_decode_q(ctx, data, ctx.n_cubes(1920, 1080, 2))
+    assert eb == reb == tb == qeb == qeb2
+    assert np.array_equal(got, ref) and np.array_equal(qgot, qref)
