@@ -785,8 +785,14 @@ __device__ __forceinline__ bool walk(const uint32_t* col, const uint8_t* lut, ui
 // 15; the maximum over a wave's 63 chunks averages 15 -- tools/walk_sim.py), and a wave runs as long as its
 // longest walk.  So each lane takes kWalkSimt steps, then the walks still going (~10 % on ramp content)
 // are queued in LDS and finished by wave 0, 64 at a time: a block pays the long tail once instead of once
-// per wave (simulated: 59 -> 26 wave-steps per block on ramp content, 71 -> 30 on uniform noise).
-constexpr uint32_t kWalkSimt = 2;
+// per wave (simulated: 59 -> 26 wave-steps per block on ramp content, 71 -> 30 on uniform noise, with 2
+// steps per lane).  Measured (profiles/r06/front/r06_wsimt*): sync pass 280 -> 241 / 246 / 247 us with 2 /
+// 4 / 1 steps per lane on ramp content, 824 / 737-744 / 863 us on uniform noise; the queue dealt to all 4
+// waves instead of wave 0: 278 / 805 us.  4 steps.
+#ifndef DCT3D_WALK_SIMT  // A/B only
+#define DCT3D_WALK_SIMT 4
+#endif
+constexpr uint32_t kWalkSimt = DCT3D_WALK_SIMT;
 __device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32_t* win, const uint8_t* lut,
                                               uint32_t* s_q, uint32_t* s_qn, int64_t first, bool own, uint32_t e,
                                               uint32_t x0, bool inv0, uint32_t stop, uint32_t limit, int64_t b0,
