@@ -830,9 +830,6 @@ __device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32
         n = n - w.na + w.nq;
         return false;
     }
-#ifdef DCT3D_DIAG_NO_CONFIRM  // diagnostic build: the walk without the confirming parse (timing only)
-    return false;
-#endif
     // rare (a dense run of long codes): the confirming pass of this chunk, inline
     bool inv2 = false;
     uint32_t x2 = 0;
@@ -947,6 +944,56 @@ __global__ __launch_bounds__(kEgBlock) void eg_sync_diag3_kernel(EgDecParams P) 
 __global__ __launch_bounds__(kEgBlock) void eg_sync_diag4_kernel(EgDecParams P) { sync_body<4>(P, 0, 1); }
 __global__ __launch_bounds__(kEgBlock) void eg_sync_diag5_kernel(EgDecParams P) { sync_body<5>(P, 0, 1); }
 #endif
+
+// Decoupled look-back over per-block descriptors (the fused front's chunk value indices):
+// desc[b] holds a flag in the top 2 bits -- 1 the block's aggregate, 2 its inclusive prefix, 3 failed --
+// and the value below (zeroed by the host before the launch).  Called by a whole wave (64 lanes) of block
+// b with the block's aggregate: publishes it, reads the predecessors 64 at a time back to an inclusive
+// prefix (waiting for any that has not published), publishes the block's inclusive prefix and returns
+// its exclusive one.  Forward progress: a block waits only for lower-numbered blocks, which the dispatcher
+// started before it; a wait longer than kLookSpin sleeps (never seen) gives up as failed, and a failed
+// block makes every later one fail (the caller then reruns without speculation).
+constexpr uint64_t kDescAgg = 1ull << 62, kDescInc = 2ull << 62, kDescFail = 3ull << 62;
+constexpr uint64_t kDescVal = (1ull << 62) - 1;
+constexpr uint32_t kLookSpin = 1u << 16;
+__device__ __forceinline__ uint64_t block_lookback(uint64_t* desc, int64_t b, uint64_t agg, bool& failed) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t excl = 0;
+    if (b > 0) {
+        if (lane == 0)
+            __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescAgg | agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t look = b - 1;
+        uint32_t spins = 0;
+        while (!failed) {
+            const int64_t i = look - (int64_t)lane;
+            const uint64_t d = i >= 0 ? __hip_atomic_load(&desc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : kDescInc;  // before block 0: an inclusive prefix of 0
+            const uint32_t flag = (uint32_t)(d >> 62);
+            const uint64_t stopm = __ballot(flag >= 2u);  // an inclusive prefix or a failure
+            const uint32_t s = stopm ? (uint32_t)__builtin_ctzll(stopm) : 64u;
+            const uint64_t upto = s >= 63u ? ~0ull : (2ull << s) - 1ull;  // lanes 0 .. s
+            if ((__ballot(flag == 0u) & upto) != 0ull) {  // a predecessor not published yet: wait
+                if (++spins > kLookSpin) failed = true;
+                __builtin_amdgcn_s_sleep(4);
+                continue;
+            }
+            if (s < 64u && __shfl(flag, s, 64) == 3u) {
+                failed = true;
+                break;
+            }
+            uint64_t v = lane <= s ? (d & kDescVal) : 0ull;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            excl += v;
+            if (s < 64u) break;
+            look -= 64;
+        }
+    }
+    if (lane == 0)
+        __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescInc | (excl + agg)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
 
 // The mark parse of one chunk from its true start sp (chunk-relative) with its first value idx0: the bit
 // position of every 32nd value.  The marks are collected in the thread's slot myk (2 bytes each, relative
@@ -1086,7 +1133,9 @@ __device__ __forceinline__ void mark_body(const EgDecParams& P) {
     const uint64_t t = (uint64_t)first + threadIdx.x;
     if (t >= P.n_chunks) return;
     // the chunk's first value index and true start: both loads in flight together, at the top issue
-    // priority (one round trip, not two behind the other blocks' parse work)
+    // priority (one round trip, not two behind the other blocks' parse work).  (Round 6: the value index
+    // by a look-back over the chunk counts instead of the scan's three launches ran the pass 295 -> 440 us,
+    // profiles/r06/front/r06_mlb: an uncached round trip on every block's critical path.)
     __builtin_amdgcn_s_setprio(3);
     const uint64_t idx0 = P.off[t];
     const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];  // the converged exits
@@ -1109,14 +1158,11 @@ __global__ __launch_bounds__(kEgBlock) void eg_mark_diag2_kernel(EgDecParams P) 
 // inclusive prefix, 3 failed -- the value below; zeroed by the host before the launch), then the mark
 // parse of each chunk from its true start (the pass-0 exit of the chunk before, in LDS).  Forward progress:
 // a block only waits for lower-numbered blocks, which the dispatcher started before it; a wait longer than
-// kFrontSpin sleeps (never seen) gives up as failed.  A failed block (a chunk that did not resolve, or the
+// kLookSpin sleeps (never seen) gives up as failed.  A failed block (a chunk that did not resolve, or the
 // wait) makes every later block fail too: no marks there, status[0] and status[2] bit 4 set, the consumer
 // skips itself and the host reruns the non-speculative front (eg_sync_kernel passes, scan, eg_mark_kernel).
 // Replaces: sync pass 0 (its window staging), the three scan launches, the mark pass's window staging and
 // its reads of the chunk offsets and exits.
-constexpr uint64_t kDescAgg = 1ull << 62, kDescInc = 2ull << 62, kDescFail = 3ull << 62;
-constexpr uint64_t kDescVal = (1ull << 62) - 1;
-constexpr uint32_t kFrontSpin = 1u << 16;
 __global__ __launch_bounds__(kEgBlock) void eg_front_kernel(EgDecParams P, uint64_t* desc, int force_fail) {
     __shared__ __attribute__((aligned(16)))
     uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock + kEgBlock * kMkSlot / 2 + kEgWaves + 6];
@@ -1179,50 +1225,12 @@ __global__ __launch_bounds__(kEgBlock) void eg_front_kernel(EgDecParams P, uint6
     // the look-back (wave 0): the counts of every chunk before the block's first
     if (wave == 0) {
         bool failed = s_misc[1] != 0;
-        uint64_t excl = 0;
-#ifdef DCT3D_FRONT_NO_LOOKBACK  // diagnostic build (timing only): the prefix from a scan run before the front
-        excl = (uint64_t)b * (kEgBlock - 1) < P.n_chunks ? P.off[b * (kEgBlock - 1)] : 0;
-        if (false) {
-#else
-        if (b > 0) {
-#endif
-            if (lane == 0)
-                __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescAgg | agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t look = b - 1;
-            uint32_t spins = 0;
-            while (!failed) {
-                const int64_t i = look - (int64_t)lane;
-                const uint64_t d = i >= 0 ? __hip_atomic_load(&desc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                          : kDescInc;  // before block 0: an inclusive prefix of 0
-                const uint32_t flag = (uint32_t)(d >> 62);
-                const uint64_t stopm = __ballot(flag >= 2u);  // an inclusive prefix or a failure
-                const uint32_t s = stopm ? (uint32_t)__builtin_ctzll(stopm) : 64u;
-                const uint64_t upto = s >= 63u ? ~0ull : (2ull << s) - 1ull;  // lanes 0 .. s
-                if ((__ballot(flag == 0u) & upto) != 0ull) {  // a predecessor not published yet: wait
-                    if (++spins > kFrontSpin) failed = true;
-                    __builtin_amdgcn_s_sleep(4);
-                    continue;
-                }
-                if (s < 64u && __shfl(flag, s, 64) == 3u) {
-                    failed = true;
-                    break;
-                }
-                uint64_t v = lane <= s ? (d & kDescVal) : 0ull;
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-                excl += v;
-                if (s < 64u) break;
-                look -= 64;
-            }
-        }
+        const uint64_t excl = block_lookback(desc, b, agg, failed);
         if (lane == 0) {
-            __hip_atomic_store(&desc[b], failed ? kDescFail : (kDescInc | (excl + agg)), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
             s_misc[0] = excl;
             s_misc[1] = failed ? 1u : 0u;
             // the total count (the scan's, status[4]: fewer values than wanted is ENODATA)
             if (!failed && b == (int64_t)gridDim.x - 1) P.status[4] = excl + agg;
-
         }
     }
     __syncthreads();

@@ -999,11 +999,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.mark_base = (uint64_t*)c->d_egd_mark.p;
     D.mark = (uint16_t*)(D.mark_base + n_mark_groups);
     D.q = nullptr;
-#ifdef DCT3D_FRONT_NO_LOOKBACK
-    if (false) {
-#else
     if (spec && c->opt_eg_fused_front) {
-#endif
         // A/B option: the fused front, one launch (eg_front_kernel); the consumer reads its verdict on the device
         const uint64_t nb = front_blocks(n_chunks);
         if ((rc = c->d_egd_desc.grow(nb * sizeof(uint64_t)))) return rc;
@@ -1046,14 +1042,6 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     S.out_cap_words = ~0ull;
     if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
-#ifdef DCT3D_FRONT_NO_LOOKBACK  // diagnostic build: the fused front after the scan, its prefixes from it
-    if (spec) {
-        const uint64_t nb = front_blocks(n_chunks);
-        if ((rc = c->d_egd_desc.grow(nb * sizeof(uint64_t)))) return rc;
-        if (launch_eg_front(D, (uint64_t*)c->d_egd_desc.p, 0, c->stream)) return DCT3D_EKERNEL;
-        return DCT3D_OK;
-    }
-#endif
     if (launch_eg_mark(D, c->stream)) return DCT3D_EKERNEL;
     return DCT3D_OK;
 }
