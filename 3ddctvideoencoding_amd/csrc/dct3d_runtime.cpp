@@ -596,13 +596,15 @@ static int chunk_stacks_for(size_t bytes_per_stack, int n_stacks) {
     return (int)(k < (size_t)half ? k : (size_t)half);
 }
 
-// compute(d_in, d_out, first_stack, stacks) enqueues one chunk's kernels on c->stream
+// compute(d_in, d_out, first_stack, stacks) enqueues one chunk's kernels on c->stream; align: chunks of a
+// multiple of this many stacks (the last one ragged)
 template <class Compute>
 static int run_pipeline(dct3d_ctx* c, int n_stacks, size_t in_per_stack, size_t out_per_stack, const void* host_in,
-                        void* host_out, Compute&& compute) {
+                        void* host_out, Compute&& compute, int align = 1) {
     int rc = ensure_pipe(c);
     if (rc) return rc;
-    const int cst = chunk_stacks_for(in_per_stack > out_per_stack ? in_per_stack : out_per_stack, n_stacks);
+    int cst = chunk_stacks_for(in_per_stack > out_per_stack ? in_per_stack : out_per_stack, n_stacks);
+    cst = (cst + align - 1) / align * align;
     const int n_chunks = (n_stacks + cst - 1) / cst;
     for (int s = 0; s < 2; s++)
         if ((in_per_stack && (rc = c->p_in[s].grow(cst * in_per_stack))) || (rc = c->p_out[s].grow(cst * out_per_stack)))
@@ -1082,6 +1084,22 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
 // re-parsing them.  out_stack0 = where stack st0 goes (the raster pointer is rebased so that the
 // kernels' global cube indices land in it).
 }  // extern "C"
+// A decode_eg_kernel launch starts on a consumer group (kMarkGroup marks = 2,048 values: the group's first
+// whole position is in mark_base, and the group's end is the next group's first): its first stack st0 must
+// put st0 * cubes-per-stack * cs on a multiple of 2,048 values.  The smallest stack count that does for a
+// w x h frame (1 at 1080p; 8 for a frame of an odd number of 8x8x8 cubes).  (Round 6: the host path's
+// chunks of stacks started anywhere, and a chunk starting inside a group parsed past its window.)
+static int eg_stack_align(const dct3d_ctx* c, int w, int h) {
+    const uint64_t per = (uint64_t)(w / c->bw) * (uint64_t)(h / c->bh) * (uint64_t)c->plan.cs;
+    const uint64_t grp = kMarkGroup * 32;
+    uint64_t a = per % grp, b = grp;  // gcd(per, grp)
+    while (a) {
+        const uint64_t t = b % a;
+        b = a;
+        a = t;
+    }
+    return (int)(grp / b);
+}
 static int decode_eg_range(dct3d_ctx* c, const EgDecParams& E, int w, int h, int st0, int ns, uint8_t* out_stack0) {
     const int D = c->bd;
     const uint64_t plane = (uint64_t)w * h;
@@ -1162,7 +1180,7 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
         batch_begin(c);
         rc = run_pipeline(c, n_stacks, 0, px, nullptr, raster, [&](const void*, void* dout, int st0, int ns) {
             return decode_eg_range(c, E, w, h, st0, ns, (uint8_t*)dout);
-        });
+        }, eg_stack_align(c, w, h));  // each chunk's first cube on a consumer group
         batch_end(c);
         if (rc) return rc;
         rc = eg_decode_status(c, E, end_bit);

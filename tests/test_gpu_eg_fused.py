@@ -410,3 +410,19 @@ def test_fused_front_option_same_results(pkg, gpu_ctx8, gpu_ctx4, depth, kind):
         qgot, qeb2 = _eg_decode_q(ctx, data, ctx.n_cubes(1920, 1080, 2))
     assert eb == reb == tb == qeb == qeb2
     assert np.array_equal(got, ref) and np.array_equal(qgot, qref)
+
+
+@pytest.mark.parametrize("depth", [8, 4])
+@pytest.mark.parametrize("w,h,stacks", [(136, 72, 3), (24, 16, 5), (8, 8, 9)])
+def test_host_decode_eg_chunks_on_groups(pkg, gpu_ctx8, gpu_ctx4, depth, w, h, stacks):
+    """The host-pointer stream decode (dct3d_decode_eg) runs the consumer in chunks of stacks; a chunk must
+    start on a consumer group (2,048 values): with stacks of 153, 6 or 1 cubes, chunks of a multiple of
+    4 / 2 / 4 stacks (8x8x4: 8 / 4 / 8).  Same raster and end bit as the two-step path (round 6: a chunk
+    starting inside a group parsed past its window)."""
+    ctx = gpu_ctx8 if depth == 8 else gpu_ctx4
+    fr = pkg.synthetic.frames(w, h, stacks * depth, kind="ramp", frame0=13)
+    data, tb = ctx.encode_eg(fr)
+    ref, reb = _decode_two_step(ctx, data, w, h, stacks)
+    got, eb = ctx.decode_eg(data, w, h, stacks)
+    assert eb == reb == tb
+    assert np.array_equal(got, ref)
