@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("host_eg,batch", [("0", "2"), ("1", "2"), ("0", "1"), ("0", "16")])
-@pytest.mark.parametrize("w,h,frames,kind", [(64, 64, 16, "ramp"), (320, 240, 24, "uniform"), (64, 48, 12, "ramp")])
+@pytest.mark.parametrize("w,h,frames,kind", [(64, 64, 16, "ramp"), (320, 240, 24, "uniform"), (64, 48, 12, "ramp"),
+                                             (136, 72, 24, "ramp")])  # 153 cubes a stack
 def test_cli_encode_decode(pkg, plan8, tmp_path, w, h, frames, kind, host_eg, batch):
     """host_eg "0": DCT + quantisation + Exp-Golomb on the device, one deflate call per batch;
     "1": the reference's split (ints over PCIe, Exp-Golomb on the host, one deflate call per stack).
