@@ -22,6 +22,7 @@ for v in "$@"; do
      python3 bench.py $args --steps 20 --warmup 5 --no-cpu-baseline --no-ceiling) > $O/prof_${label}_$r.log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "rocprof $label rc=$rc"; tail -3 $O/prof_${label}_$r.log; exit $rc; }
   f=$(find $O/prof_${label}_$r -name '*kernel_stats.csv' | head -1); cp "$f" $O/kernel_stats_${label}_$r.csv
+  [ -z "$KEEP_TRACE" ] && rm -rf $O/prof_${label}_$r  # the traces: 10+ MiB each (gpurun copies back <= 64 MiB)
   grep '^{"metric"' $O/prof_${label}_$r.log | tail -1 > $O/bench_${label}_$r.json
   python3 - "$O/kernel_stats_${label}_$r.csv" "$O/bench_${label}_$r.json" "$label" "${KMATCH:-eg_|front}" <<'PY'
 import csv, json, re, sys
