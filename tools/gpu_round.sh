@@ -31,6 +31,7 @@ for c in ${CONFIGS:-c2 c2u c3 c4}; do
        python3 bench.py ${CFG[$c]} --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-ceiling > $OUT/prof_$c.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { tail -5 $OUT/prof_$c.log; stop $rc prof_$c; }
     f=$(find $OUT/prof_$c -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" $OUT/kernel_stats_$c.csv
+    [ -z "$KEEP_TRACE" ] && rm -rf $OUT/prof_$c  # the traces (10+ MiB each; gpurun copies back <= 64 MiB)
   fi
 done
 exit 0
