@@ -308,9 +308,13 @@ __device__ __forceinline__ void dec_store_tile(const DecodeParams& P, char* wl, 
 // reload(g, cf, lane) re-reads cube g's dequantised coefficients for the rare exact replay.
 // PG: butterflies per pin group (1: one at a time, 2 / 4: that many interleaved, 0: no pins)
 // CODES: the staging holds Exp-Golomb codes, not values (decode_eg_kernel): v = code >> 1, negative when the
-// code is odd -- the sign goes into the converted magnitude's sign bit (one v_lshl_or) and the product is the same exact
-// q * step, except that code 1 (value 0) gives -0.0 (|cf| in L1, and the outputs' truncation and
-// certificate, do not see a zero's sign; the exact replay reloads the values).
+// code is odd.  |q| * step in 32-bit integers (v_mul_u32_u24: exact while |q| < 2^15, < 2^22), the lane's
+// L1 as their exact integer sum (< 2^27), the fp64 value by one exact conversion with the sign put into its
+// sign bit (one v_lshl_or): the same cf as the fp64 product, except that code 1 (value 0) gives -0.0 (the
+// outputs' truncation and certificate do not see a zero's sign), at 4 fewer VALU cycles per value than an
+// fp64 product and fp64 L1 sum.  A lane holding a code >= 2^16 (|q| >= 2^15: a code of 33+ bits, never
+// written for 8-bit frames) reports L1 = inf, so its whole cube goes to the exact replay, which reloads the
+// values from the stream.
 template <int D, int PG, bool LOOP = false, bool CODES = false, class AfterA, class Reload>
 __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int lane, uint32_t cube0,
                                             AfterA&& after_a, const Reload& reload) {
@@ -334,32 +338,44 @@ __device__ __forceinline__ void decode_tile(const DecodeParams& P, char* wl, int
     {
         int sb = 5 * (4 * h + k);  // step = sb + 5 (e + ky); DC (e = ky = 0): 1
         if constexpr (LOOP) asm volatile("" : "+v"(sb));  // (dec_store_tile's LOOP)
-        double stp[11];
-        stp[0] = (double)max(sb, 1);
-#pragma unroll
-        for (int j = 1; j < 11; j++) stp[j] = (double)(sb + 5 * j);
         const char* src = wl + c * G::SA_C + k * G::SA_F + h * 16;
         int4 raw[8];  // all eight LDS reads in flight before the first use
 #pragma unroll
         for (int ky = 0; ky < 8; ky++) raw[ky] = *(const int4*)(src + ky * 32);
-        double l1 = 0.0;
+        if constexpr (CODES) {
+            uint32_t l1 = 0, any = 0;
 #pragma unroll
-        for (int ky = 0; ky < 8; ky++) {
-            const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
+            for (int ky = 0; ky < 8; ky++) {
+                const uint32_t vv[4] = {(uint32_t)raw[ky].x, (uint32_t)raw[ky].y, (uint32_t)raw[ky].z, (uint32_t)raw[ky].w};
+                any |= vv[0] | vv[1] | vv[2] | vv[3];
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                if constexpr (CODES) {
-                    const uint32_t cd = (uint32_t)vv[e];
-                    uint2 m = __builtin_bit_cast(uint2, (double)(cd >> 1));
-                    asm("v_lshl_or_b32 %0, %1, 31, %2" : "=v"(m.y) : "v"(cd), "v"(m.y));  // (the compiler: 2 VALU)
-                    b[ky][e] = __dmul_rn(__builtin_bit_cast(double, m), stp[e + ky]);
-                } else {
-                    b[ky][e] = __dmul_rn((double)vv[e], stp[e + ky]);
+                for (int e = 0; e < 4; e++) {
+                    const uint32_t st = (e + ky) ? (uint32_t)(sb + 5 * (e + ky)) : (uint32_t)max(sb, 1);
+                    const uint32_t ms = __umul24(vv[e] >> 1, st);  // |q| * step
+                    l1 += ms;
+                    uint2 m = __builtin_bit_cast(uint2, (double)ms);
+                    asm("v_lshl_or_b32 %0, %1, 31, %2" : "=v"(m.y) : "v"(vv[e]), "v"(m.y));  // the sign: the code odd
+                    b[ky][e] = __builtin_bit_cast(double, m);
                 }
-                l1 = __dadd_rn(l1, __builtin_fabs(b[ky][e]));
             }
+            l1_f = any < 0x10000u ? (float)l1 : __builtin_inff();
+        } else {
+            double stp[11];
+            stp[0] = (double)max(sb, 1);
+#pragma unroll
+            for (int j = 1; j < 11; j++) stp[j] = (double)(sb + 5 * j);
+            double l1 = 0.0;
+#pragma unroll
+            for (int ky = 0; ky < 8; ky++) {
+                const int vv[4] = {raw[ky].x, raw[ky].y, raw[ky].z, raw[ky].w};
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    b[ky][e] = __dmul_rn((double)vv[e], stp[e + ky]);
+                    l1 = __dadd_rn(l1, __builtin_fabs(b[ky][e]));
+                }
+            }
+            l1_f = (float)l1;
         }
-        l1_f = (float)l1;
     }
     after_a();
     // L1 over the cube's lanes (k bits, then bit 4): DPP within the row, one permlane16 swap across
