@@ -93,28 +93,67 @@ __global__ __launch_bounds__(kEgBlock) void eg_scan_reduce_kernel(EgParams P) {
     }
 }
 
-// one block: exclusive scan of the chunk sums (offset by the carried bits), total, capacity check
-__global__ __launch_bounds__(1024) void eg_scan_top_kernel(EgParams P, uint32_t n_chunks) {
-    __shared__ uint64_t buf[1024];
-    uint64_t carry = P.carry_bits;
-    for (uint32_t c0 = 0; c0 < n_chunks; c0 += 1024) {
-        const uint32_t i = c0 + threadIdx.x;
-        const uint64_t v = i < n_chunks ? P.bsum[i] : 0;
-        buf[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-            const uint64_t t = threadIdx.x >= (unsigned)o ? buf[threadIdx.x - o] : 0;
-            __syncthreads();
-            buf[threadIdx.x] += t;
-            __syncthreads();
+// The stream decode's reduce (round 6: replaces the apply kernel and its 8-byte offset per chunk): block b
+// sums the counts of chunks 4096 b .. 4096 b + 4095 into bsum[b] (then scanned by eg_scan_top_kernel) and
+// each 256 of them into part[16 b + i] (thread t holds the 16 consecutive counts 16 t ..: a part is 16
+// lanes).  The mark pass adds the parts before its block and scans its own 256 counts.
+__global__ __launch_bounds__(kEgBlock) void eg_dscan_reduce_kernel(EgDecParams P) {
+    static_assert(kScanChunk == 16 * kEgBlock && kEgBlock == 256, "16 counts per thread, 16 parts per block");
+    __shared__ uint32_t wsum[kEgWaves];
+    const uint64_t base = (uint64_t)blockIdx.x * kScanChunk + threadIdx.x * 16u;
+    uint32_t s = 0;
+    if (base + 16 <= P.n_chunks) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 t = *(const uint4*)(P.count + base + 4 * q);
+            s += t.x + t.y + t.z + t.w;
         }
-        if (i < n_chunks) P.bsum[i] = carry + buf[threadIdx.x] - v;
-        carry += buf[1023];
-        __syncthreads();
+    } else {
+        for (uint32_t i = 0; i < 16; i++) s += base + i < P.n_chunks ? P.count[base + i] : 0u;
+    }
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o, 64);  // the part: 16 lanes
+    if ((lane & 15) == 0) P.part[(uint64_t)blockIdx.x * 16 + wave * 4 + lane / 16] = s;
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane == 0) wsum[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) P.bsum[blockIdx.x] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// one block: exclusive scan of the chunk sums (offset by the carried bits), total, capacity check.  Thread t
+// owns the consecutive sums t K .. t K + K - 1 (K = ceil(n / 1024)): their serial sum, one block scan of the
+// 1,024 sums (in the wave by shuffles, the 16 waves' totals through LDS), then its prefixes written back.
+// (Round 6; a Hillis-Steele pass per 1,024 sums before: 20 barriers each, 5 / 9 us per c8 step.)
+__global__ __launch_bounds__(1024) void eg_scan_top_kernel(EgParams P, uint32_t n_chunks) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t K = (n_chunks + 1023) / 1024;
+    const uint32_t i0 = threadIdx.x * K;
+    uint64_t s = 0;
+    for (uint32_t i = i0; i < i0 + K && i < n_chunks; i++) s += P.bsum[i];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t incl = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t run = (uint64_t)P.carry_bits + incl - s, total = P.carry_bits;
+    for (uint32_t w = 0; w < 16; w++) {
+        run += w < wave ? wsum[w] : 0u;
+        total += wsum[w];
+    }
+    for (uint32_t i = i0; i < i0 + K && i < n_chunks; i++) {
+        const uint64_t v = P.bsum[i];
+        P.bsum[i] = run;
+        run += v;
     }
     if (threadIdx.x == 0) {
-        P.status[0] = carry;  // total bits including the carried ones
-        if ((carry + 31) / 32 > P.out_cap_words) atomicOr((unsigned int*)&P.status[1], 1u);
+        P.status[0] = total;  // total bits including the carried ones
+        if ((total + 31) / 32 > P.out_cap_words) atomicOr((unsigned int*)&P.status[1], 1u);
     }
 }
 
@@ -1112,10 +1151,11 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
 // exit of the chunk before), its first value index from the scan.
 template <int DIAG>
 __device__ __forceinline__ void mark_body(const EgDecParams& P) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock * kMkSlot / 2 + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock * kMkSlot / 2 + 1 + 6];
     uint8_t* const s_lut = (uint8_t*)lds;
     uint32_t* const win = lds + kLutBytes / 4;
     uint16_t* const s_mk = (uint16_t*)(win + kColBytes / 4);
+    uint32_t* const s_ws = (uint32_t*)(s_mk + kEgBlock * kMkSlot) + 1;  // the waves' count sums, then the base
     copy_lut(s_lut);
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
     // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
@@ -1124,22 +1164,43 @@ __device__ __forceinline__ void mark_body(const EgDecParams& P) {
         return;
     }
     const int64_t first = (int64_t)blockIdx.x * kEgBlock;
+    const uint64_t t = (uint64_t)first + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the chunk's count and true start, and wave 0's parts of the chunks before the block within its 4,096
+    // (eg_dscan_reduce_kernel), in flight together at the top issue priority with the window's loads
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t cnt = t < P.n_chunks ? P.count[t] : 0u;
+    const uint64_t s = t == 0 ? P.start_bit : (t < P.n_chunks ? P.exit_in[t - 1] : kNoExit);  // the converged exits
+    const uint32_t pj = (uint32_t)(blockIdx.x & 15u);
+    const uint32_t pv = (wave == 0 && lane < pj) ? P.part[(uint64_t)blockIdx.x - pj + lane] : 0u;
+    const uint64_t bb = P.bsum[blockIdx.x >> 4];
+    __builtin_amdgcn_s_setprio(0);
     stage_columns(P, win, first);
+    // the block's exclusive scan of the counts: in the wave by shuffles, across the waves through LDS
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += v;
+    }
+    if (lane == 63) s_ws[wave] = incl;
+    if (wave == 0) {
+        uint32_t ps = pv;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) ps += __shfl_xor(ps, o, 64);
+        if (lane == 0) s_ws[kEgWaves] = ps;
+    }
     __syncthreads();
     if (DIAG == 1) {
         if (column(win)[0] == 0x12345678u && P.n_chunks == 0) P.count[0] = 1u;  // keeps the staging
         return;
     }
-    const uint64_t t = (uint64_t)first + threadIdx.x;
     if (t >= P.n_chunks) return;
-    // the chunk's first value index and true start: both loads in flight together, at the top issue
-    // priority (one round trip, not two behind the other blocks' parse work).  (Round 6: the value index
-    // by a look-back over the chunk counts instead of the scan's three launches ran the pass 295 -> 440 us,
-    // profiles/r06/front/r06_mlb: an uncached round trip on every block's critical path.)
-    __builtin_amdgcn_s_setprio(3);
-    const uint64_t idx0 = P.off[t];
-    const uint64_t s = t == 0 ? P.start_bit : P.exit_in[t - 1];  // the converged exits
-    __builtin_amdgcn_s_setprio(0);
+    uint64_t idx0 = bb + s_ws[kEgWaves] + (incl - cnt);
+#pragma unroll
+    for (uint32_t w = 0; w < (uint32_t)kEgWaves; w++) idx0 += w < wave ? s_ws[w] : 0u;
+    // (Round 6: the value index by a look-back over the chunk counts instead of the scan ran the pass
+    // 295 -> 440 us, profiles/r06/front/r06_mlb: an uncached round trip on every block's critical path.)
     if (idx0 >= P.n_values) return;
     if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
     const int64_t b0 = (int64_t)P.start_bit + (int64_t)t * (int64_t)kChunkBits;
@@ -1393,6 +1454,13 @@ int launch_eg_front(const EgDecParams& P, uint64_t* desc, int force_fail, hipStr
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+int launch_eg_dscan(const EgDecParams& P, const EgParams& S, hipStream_t st) {
+    if (P.n_chunks == 0) return 0;
+    const uint64_t nb = (P.n_chunks + kScanChunk - 1) / kScanChunk;
+    hipLaunchKernelGGL(eg_dscan_reduce_kernel, dim3((uint32_t)nb), dim3(kEgBlock), 0, st, P);
+    hipLaunchKernelGGL(eg_scan_top_kernel, dim3(1), dim3(1024), 0, st, S, (uint32_t)nb);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 int launch_eg_mark(const EgDecParams& P, hipStream_t st) {
     if (P.n_chunks == 0) return 0;
 #ifdef DCT3D_DIAG_FRONT  // diagnostic build: the mark pass's parts before it (timing only)

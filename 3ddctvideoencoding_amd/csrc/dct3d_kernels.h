@@ -113,7 +113,11 @@ struct EgDecParams {
     uint64_t* exit_in;         // previous iteration's exits (UINT64_MAX: the parse ended invalid)
     uint64_t* exit_out;
     uint32_t* count;           // codewords per chunk
-    uint64_t* off;             // value index of each chunk's first codeword (scan)
+    uint64_t* off;             // (unused by the stream decode since round 6: the mark pass scans its block)
+    // the scan of the counts (launch_eg_dscan): bsum[b] = the value index of chunk 4096 b's first codeword,
+    // part[i] = the codewords of chunks 256 i .. 256 i + 255
+    uint64_t* bsum;
+    uint32_t* part;
     // [0] changed / first invalid chunk, [1] end bit, [2] flags (1 corrupt, 2 short, 4 rerun), [3] a code of
     // 33+ bits seen (mark pass; the consumers then parse with CHECK); zeroed with the other words by
     // eg_decode_front's memset before every pass
@@ -176,6 +180,9 @@ int launch_eg_sync(const EgDecParams& P, int iteration, int resolve, hipStream_t
 int launch_eg_scan(const EgParams& P, hipStream_t st);   // scan of P.bits[0..n_cubes) into P.off / P.status[0]
 int launch_eg_decode_write(int D, const EgDecParams& P, hipStream_t st);  // mark pass + emit
 int launch_eg_mark(const EgDecParams& P, hipStream_t st);
+// the stream decode's scan of the chunk counts: P.bsum (exclusive, per 4,096 chunks), P.part (per 256) and
+// the total (S.status[0]); S: the scan's status words and the generic scan's parameters
+int launch_eg_dscan(const EgDecParams& P, const EgParams& S, hipStream_t st);
 // the fused front (resolving sync pass + scan + mark pass in one launch; desc: front_blocks(n_chunks) zeroed
 // words); a chunk that does not resolve: status[2] bit 4 (rerun without speculation)
 uint64_t front_blocks(uint64_t n_chunks);

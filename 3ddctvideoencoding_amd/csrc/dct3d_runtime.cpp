@@ -980,7 +980,7 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     const uint64_t n_scan = (n_chunks + 4095) / 4096;
     int rc = c->d_egd_exit.grow(2 * n_chunks * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_bits.grow(n_chunks * sizeof(uint32_t));
-    if (!rc) rc = c->d_eg_off.grow(n_chunks * sizeof(uint64_t));
+    if (!rc) rc = c->d_eg_off.grow(16 * n_scan * sizeof(uint32_t));  // the scan's parts (launch_eg_dscan)
     if (!rc) rc = c->d_eg_bsum.grow((n_scan + 1) * sizeof(uint64_t));
     const uint64_t n_marks = n_cubes * (uint64_t)c->plan.cs / 32;
     const uint64_t n_mark_groups = n_marks / kMarkGroup + 1;
@@ -996,7 +996,9 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.diag = (const uint16_t*)c->d_diag.p;
     uint64_t* ex[2] = {(uint64_t*)c->d_egd_exit.p, (uint64_t*)c->d_egd_exit.p + n_chunks};
     D.count = (uint32_t*)c->d_eg_bits.p;
-    D.off = (uint64_t*)c->d_eg_off.p;
+    D.off = nullptr;
+    D.part = (uint32_t*)c->d_eg_off.p;
+    D.bsum = (uint64_t*)c->d_eg_bsum.p;
     D.status = (uint64_t*)c->d_egd_status.p;
     D.mark_base = (uint64_t*)c->d_egd_mark.p;
     D.mark = (uint16_t*)(D.mark_base + n_mark_groups);
@@ -1038,11 +1040,10 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     memset(&S, 0, sizeof(S));
     S.n_cubes = n_chunks;
     S.bits = D.count;
-    S.off = D.off;
-    S.bsum = (uint64_t*)c->d_eg_bsum.p;
+    S.bsum = D.bsum;
     S.status = D.status + 4;  // zeroed with the decode's words
     S.out_cap_words = ~0ull;
-    if (launch_eg_scan(S, c->stream)) return DCT3D_EKERNEL;
+    if (launch_eg_dscan(D, S, c->stream)) return DCT3D_EKERNEL;
     D.exit_in = ex[cur];  // the converged exits
     if (launch_eg_mark(D, c->stream)) return DCT3D_EKERNEL;
     return DCT3D_OK;
