@@ -125,6 +125,12 @@ struct EgDecParams {
     uint16_t* mark;            // [n_values / 32] bit position of every 32nd value, low 16 bits
     uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output
+    // (decode_eg_kernel, optional) the host's pinned copy of status[0..5], written by block 0 as it starts
+    // (every word is final by then): the call's verdict needs no copy kernel behind the consumer
+    uint64_t* status_host;
+    // (decode_eg_kernel, optional) the ctx's other status slot, zeroed by block 0 for the next call (whose
+    // front then needs no memset)
+    uint64_t* status_clear;
 };
 
 // Fused encode + Exp-Golomb (dct3d_encode_eg_dev): the encode kernel's transform / quantise /

@@ -96,8 +96,13 @@ struct dct3d_ctx {
     // Exp-Golomb decode: chunk exits (two passes' worth), decode status, staged stream / raster
     // (d_egd_status: the decode's four status words, then the scan's two -- one read-back per call)
     DevBuf d_egd_exit, d_egd_status, d_egd_in, d_egd_raster, d_egd_mark, d_egd_desc;
+    // d_egd_status holds two slots of the words; calls alternate between them, and the fused decode's
+    // consumer zeroes the other slot for the next call (clean: known zero, no memset needed)
+    int egd_slot = 0;
+    bool egd_clean[2] = {true, true};
     // pinned host words the entropy stages' status lands in (one DMA read-back, not a pageable copy)
     uint64_t* h_status = nullptr;
+    uint64_t* h_status_dev = nullptr;  // its device-side address (decode_eg_kernel writes the words there)
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
     hipStream_t s_up = nullptr, s_down = nullptr;
     hipEvent_t pe_in[2] = {}, pe_done[2] = {};
@@ -152,9 +157,20 @@ const char* dct3d_strerror(int code) {
 
 // the status words of an entropy stage (device, written by its kernels on the context stream): one
 // asynchronous copy into the pinned words, then the stream's completion
+// The end of a synchronous call: the stream polled for a while before blocking (a blocking wait took
+// ~15-40 us to return after the stream's last kernel, profiles/r06/gaps/), so that the caller's next
+// call reaches the device sooner.
+static int stream_wait(dct3d_ctx* c) {
+    for (int i = 0; i < 20000; i++) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) return DCT3D_OK;
+        if (e != hipErrorNotReady) return DCT3D_EDEVICE;
+    }
+    return hipStreamSynchronize(c->stream) == hipSuccess ? DCT3D_OK : DCT3D_EDEVICE;
+}
 static int read_status(dct3d_ctx* c, const void* d_status, size_t bytes, uint64_t* out) {
     if (hipMemcpyAsync(c->h_status, d_status, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
+        stream_wait(c))
         return DCT3D_EDEVICE;
     memcpy(out, c->h_status, bytes);
     return DCT3D_OK;
@@ -248,11 +264,13 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         rc = upload(c->d_diag, diag.data(), diag.size() * sizeof(uint16_t));
     }
     if (!rc) rc = c->d_eg_status.grow(16);
-    if (!rc) rc = c->d_egd_status.grow(kEgdStatusBytes);
+    if (!rc) rc = c->d_egd_status.grow(2 * kEgdStatusBytes);
+    if (!rc && hipMemset(c->d_egd_status.p, 0, 2 * kEgdStatusBytes) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc && hipHostMalloc((void**)&c->h_status, kEgdStatusBytes, hipHostMallocDefault) != hipSuccess) {
         c->h_status = nullptr;
         rc = DCT3D_ENOMEM;
     }
+    if (!rc && hipHostGetDevicePointer((void**)&c->h_status_dev, c->h_status, 0) != hipSuccess) c->h_status_dev = nullptr;
     if (rc) {
         dct3d_ctx_destroy(c);
         return rc;
@@ -999,15 +1017,20 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     D.off = nullptr;
     D.part = (uint32_t*)c->d_eg_off.p;
     D.bsum = (uint64_t*)c->d_eg_bsum.p;
-    D.status = (uint64_t*)c->d_egd_status.p;
+    uint64_t* const st = (uint64_t*)c->d_egd_status.p + 6 * c->egd_slot;  // this call's words
+    const bool clean = c->egd_clean[c->egd_slot];
+    c->egd_clean[c->egd_slot] = false;
+    D.status = st;
+    D.status_clear = nullptr;
     D.mark_base = (uint64_t*)c->d_egd_mark.p;
     D.mark = (uint16_t*)(D.mark_base + n_mark_groups);
     D.q = nullptr;
+    D.status_host = nullptr;
     if (spec && c->opt_eg_fused_front) {
         // A/B option: the fused front, one launch (eg_front_kernel); the consumer reads its verdict on the device
         const uint64_t nb = front_blocks(n_chunks);
         if ((rc = c->d_egd_desc.grow(nb * sizeof(uint64_t)))) return rc;
-        if (hipMemsetAsync(c->d_egd_status.p, 0, kEgdStatusBytes, c->stream) != hipSuccess ||
+        if ((!clean && hipMemsetAsync(st, 0, kEgdStatusBytes, c->stream) != hipSuccess) ||
             hipMemsetAsync(c->d_egd_desc.p, 0, nb * sizeof(uint64_t), c->stream) != hipSuccess)
             return DCT3D_EDEVICE;
         if (launch_eg_front(D, (uint64_t*)c->d_egd_desc.p, c->opt_eg_force_retry ? 1 : 0, c->stream)) return DCT3D_EKERNEL;
@@ -1019,19 +1042,19 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     const bool resolve = !c->opt_eg_no_resolve;
     int cur = 0;
     for (uint64_t it = 0; it <= n_chunks + 1; it++) {
-        if (hipMemsetAsync(c->d_egd_status.p, 0, kEgdStatusBytes, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+        if (!(it == 0 && clean) && hipMemsetAsync(st, 0, kEgdStatusBytes, c->stream) != hipSuccess) return DCT3D_EDEVICE;
         D.exit_in = ex[cur];
         D.exit_out = ex[cur ^ 1];
         if (launch_eg_sync(D, (int)(it < 2 ? it : 1), resolve, c->stream)) return DCT3D_EKERNEL;
         cur ^= 1;
         if (it == 0 && !resolve) continue;
         if (it == 0 && spec) {  // speculative front: the verdict is read on the device (eg_mark_kernel)
-            if (c->opt_eg_force_retry && hipMemsetAsync(c->d_egd_status.p, 0x01, 1, c->stream) != hipSuccess)
+            if (c->opt_eg_force_retry && hipMemsetAsync(st, 0x01, 1, c->stream) != hipSuccess)
                 return DCT3D_EDEVICE;
             break;
         }
         uint64_t changed = 0;
-        if (read_status(c, c->d_egd_status.p, 8, &changed)) return DCT3D_EDEVICE;
+        if (read_status(c, st, 8, &changed)) return DCT3D_EDEVICE;
         if (!changed) break;
         if (it == n_chunks + 1) return DCT3D_EINVAL;  // cannot happen: every pass fixes one more chunk
     }
@@ -1049,10 +1072,17 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
     return DCT3D_OK;
 }
 
-// waits for the stream; the decode's verdict (corrupt: EINVAL, too short: ENODATA) and end bit
+// waits for the stream; the decode's verdict (corrupt: EINVAL, too short: ENODATA) and end bit (the
+// consumer wrote the words to the host itself when D.status_host is set)
 static int eg_decode_status(dct3d_ctx* c, const EgDecParams& D, uint64_t* end_bit) {
     uint64_t w[6] = {0, 0, 0, 0, 0, 0};
-    if (read_status(c, c->d_egd_status.p, kEgdStatusBytes, w)) return DCT3D_EDEVICE;
+    if (D.status_host) {
+        if (stream_wait(c)) return DCT3D_EDEVICE;
+        memcpy(w, c->h_status, kEgdStatusBytes);
+    } else if (read_status(c, D.status, kEgdStatusBytes, w)) {
+        return DCT3D_EDEVICE;
+    }
+    c->egd_slot ^= 1;  // the next call's words
     const uint64_t* st = w;         // the decode's words
     const uint64_t* total = w + 4;  // the scan's: total bits, flags
     if (st[2] & 4) return kEgRetry;  // a speculative front whose pass 0 did not resolve: rerun
@@ -1153,7 +1183,10 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     for (int spec = 1;; spec = 0) {
         EgDecParams E;
         if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E, spec && !c->opt_eg_no_resolve))) return rc;
+        E.status_host = c->h_status_dev;  // the consumer hands the verdict to the host (nullptr: a copy)
+        E.status_clear = (uint64_t*)c->d_egd_status.p + 6 * (c->egd_slot ^ 1);  // and zeroes the next call's
         if ((rc = decode_eg_range(c, E, w, h, 0, n_stacks, d_raster))) return rc;
+        c->egd_clean[c->egd_slot ^ 1] = true;
         rc = eg_decode_status(c, E, end_bit);
         if (rc != kEgRetry || !spec) return rc == kEgRetry ? DCT3D_EDEVICE : rc;
     }
