@@ -315,6 +315,10 @@ __global__ __launch_bounds__(kEgBlock) void eg_write_kernel(EgParams P) {
 // thread per cube: the first word of cube g = its head | the previous cube's tail when they share the
 // word (| the carried partial byte for g = 0); the last word (tail) unless the next cube shares it
 __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
+    if (blockIdx.x == 0 && threadIdx.x < 2) {
+        if (P.status_host) P.status_host[threadIdx.x] = P.status[threadIdx.x];
+        if (P.status_clear) P.status_clear[threadIdx.x] = 0u;
+    }
     if (P.status[1] != 0) return;
     const uint64_t g = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (g >= P.n_cubes) return;

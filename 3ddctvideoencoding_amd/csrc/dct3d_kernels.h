@@ -91,6 +91,10 @@ struct EgParams {
     uint32_t* out;             // output words (memory byte order), capacity out_cap_words
     uint64_t out_cap_words;
     uint32_t carry_bits, carry_byte;
+    // (eg_stitch_kernel, optional) the host's pinned copy of status[0..1], written by block 0, and the other
+    // of the ctx's two status slots, zeroed for the next call (no copy kernel and no memset per call)
+    uint64_t* status_host;
+    uint64_t* status_clear;
 };
 
 // Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)

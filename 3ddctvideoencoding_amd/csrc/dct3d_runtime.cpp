@@ -100,6 +100,9 @@ struct dct3d_ctx {
     // consumer zeroes the other slot for the next call (clean: known zero, no memset needed)
     int egd_slot = 0;
     bool egd_clean[2] = {true, true};
+    // the same for the encode stream's two status words (d_eg_status: two slots of 16 bytes)
+    int eg_slot = 0;
+    bool eg_clean[2] = {true, true};
     // pinned host words the entropy stages' status lands in (one DMA read-back, not a pageable copy)
     uint64_t* h_status = nullptr;
     uint64_t* h_status_dev = nullptr;  // its device-side address (decode_eg_kernel writes the words there)
@@ -174,6 +177,33 @@ static int read_status(dct3d_ctx* c, const void* d_status, size_t bytes, uint64_
         return DCT3D_EDEVICE;
     memcpy(out, c->h_status, bytes);
     return DCT3D_OK;
+}
+
+// The encode stream's status words for this call (zeroed: by a memset unless the last call's stitch kernel
+// cleared this slot), and the kernel-side hand-off (EgParams::status_host / status_clear).
+static uint64_t* eg_status_begin(dct3d_ctx* c, int* rc) {
+    uint64_t* st = (uint64_t*)c->d_eg_status.p + 2 * c->eg_slot;
+    const bool clean = c->eg_clean[c->eg_slot];
+    c->eg_clean[c->eg_slot] = false;
+    *rc = !clean && hipMemsetAsync(st, 0, 16, c->stream) != hipSuccess ? DCT3D_EDEVICE : DCT3D_OK;
+    return st;
+}
+static void eg_status_handoff(dct3d_ctx* c, EgParams& P) {
+    P.status_host = c->h_status_dev;
+    P.status_clear = (uint64_t*)c->d_eg_status.p + 2 * (c->eg_slot ^ 1);
+}
+// after the stitch kernel was enqueued with the hand-off: its words in the pinned buffer
+static int eg_status_end(dct3d_ctx* c, bool handoff, const uint64_t* st, uint64_t* out) {
+    int rc;
+    if (handoff) {
+        c->eg_clean[c->eg_slot ^ 1] = true;
+        rc = stream_wait(c);
+        if (!rc) memcpy(out, c->h_status, 16);
+    } else {
+        rc = read_status(c, st, 16, out);
+    }
+    c->eg_slot ^= 1;
+    return rc;
 }
 
 static int upload(DevBuf& b, const void* src, size_t bytes) {
@@ -263,7 +293,8 @@ int dct3d_ctx_create(int device, int block_w, int block_h, int block_d, dct3d_ct
         diagonal_order(block_w, block_h, block_d, diag.data());
         rc = upload(c->d_diag, diag.data(), diag.size() * sizeof(uint16_t));
     }
-    if (!rc) rc = c->d_eg_status.grow(16);
+    if (!rc) rc = c->d_eg_status.grow(32);
+    if (!rc && hipMemset(c->d_eg_status.p, 0, 32) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc) rc = c->d_egd_status.grow(2 * kEgdStatusBytes);
     if (!rc && hipMemset(c->d_egd_status.p, 0, 2 * kEgdStatusBytes) != hipSuccess) rc = DCT3D_EDEVICE;
     if (!rc && hipHostMalloc((void**)&c->h_status, kEgdStatusBytes, hipHostMallocDefault) != hipSuccess) {
@@ -807,15 +838,17 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     if (!rc) rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t));
     if (!rc) rc = c->d_eg_ht.grow(2 * n_cubes * sizeof(uint32_t));
     if (rc) return rc;
-    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
-    EgParams P;
+    uint64_t* const sw = eg_status_begin(c, &rc);
+    if (rc) return rc;
+    EgParams P{};
     P.q = d_q;
     P.n_cubes = n_cubes;
     P.diag = (const uint16_t*)c->d_diag.p;
     P.bits = (uint32_t*)c->d_eg_bits.p;
     P.off = (uint64_t*)c->d_eg_off.p;
     P.bsum = (uint64_t*)c->d_eg_bsum.p;
-    P.status = (uint64_t*)c->d_eg_status.p;
+    P.status = sw;
+    eg_status_handoff(c, P);  // the stitch kernel (the last of launch_eg_encode) hands the words over
     P.head = (uint32_t*)c->d_eg_ht.p;
     P.tail = (uint32_t*)c->d_eg_ht.p + n_cubes;
     P.out = d_out;
@@ -824,7 +857,7 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     P.carry_byte = carry_byte;
     if (launch_eg_encode(c->bd, P, c->stream)) return DCT3D_EKERNEL;
     uint64_t st[2] = {0, 0};
-    if (read_status(c, c->d_eg_status.p, 16, st)) return DCT3D_EDEVICE;
+    if (eg_status_end(c, true, sw, st)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     if (st[1] & 2) return DCT3D_EINVAL;
     if (st[1] & 1) return DCT3D_ENOSPC;
@@ -870,7 +903,8 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
         (rc = c->d_eg_off.grow(n_seg * sizeof(uint64_t))) || (rc = c->d_eg_bsum.grow((n_chunks + 1) * sizeof(uint64_t))) ||
         (rc = c->d_eg_ht.grow(2 * n_seg * sizeof(uint32_t))))
         return rc;
-    if (hipMemsetAsync(c->d_eg_status.p, 0, 16, c->stream) != hipSuccess) return DCT3D_EDEVICE;
+    uint64_t* const sw = eg_status_begin(c, &rc);
+    if (rc) return rc;
     const uint64_t plane = (uint64_t)w * h;
     EncodeParams P{};
     P.raster = d_raster;
@@ -896,14 +930,15 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     E.slot = (uint32_t*)c->d_egf_slot.p;
     E.seg_cap = seg_cap;
     E.seg_bits = (uint32_t*)c->d_eg_bits.p;
-    EgParams G;
+    EgParams G{};
     G.q = nullptr;
     G.n_cubes = n_seg;  // segments
     G.diag = E.diag;
     G.bits = E.seg_bits;
     G.off = (uint64_t*)c->d_eg_off.p;
     G.bsum = (uint64_t*)c->d_eg_bsum.p;
-    G.status = (uint64_t*)c->d_eg_status.p;
+    G.status = sw;
+    eg_status_handoff(c, G);  // the stitch kernel (the last of launch_eg_compact) hands the words over
     G.head = (uint32_t*)c->d_eg_ht.p;
     G.tail = (uint32_t*)c->d_eg_ht.p + n_seg;
     G.out = (uint32_t*)d_out;
@@ -918,7 +953,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (launch_eg_compact(G, E.slot, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
-    if (read_status(c, c->d_eg_status.p, 16, st)) return DCT3D_EDEVICE;
+    if (eg_status_end(c, true, sw, st)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     if (st[1] & 1) return DCT3D_ENOSPC;
