@@ -836,10 +836,12 @@ __device__ __forceinline__ bool walk(const uint32_t* col, const uint8_t* lut, ui
 #define DCT3D_WALK_SIMT 4
 #endif
 constexpr uint32_t kWalkSimt = DCT3D_WALK_SIMT;
+// qcap: the queue's entries; a walk that finds it full finishes in its own lane (rare: ~10 % of the chunks
+// queue, and the sync pass's queue holds 60 of its 255).
 __device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32_t* win, const uint8_t* lut,
                                               uint32_t* s_q, uint32_t* s_qn, int64_t first, bool own, uint32_t e,
                                               uint32_t x0, bool inv0, uint32_t stop, uint32_t limit, int64_t b0,
-                                              uint32_t& n, uint32_t& x) {
+                                              uint32_t& n, uint32_t& x, uint32_t qcap = kEgBlock) {
     const uint32_t* col = column(win);
     x = inv0 ? ~0u : x0;
     const bool walking = own && e < kMeetBits;  // (e = ~0u: not walking)
@@ -847,11 +849,16 @@ __device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32
     uint32_t slot = ~0u;
     if (walking && !walk(col, lut, limit, w, kWalkSimt)) {
         slot = atomicAdd(s_qn, 1u);
-        s_q[2 * slot] = threadIdx.x | (w.pa << 8) | (w.pq << 16) | (w.na << 24);  // all < 256
-        s_q[2 * slot + 1] = w.nq;
+        if (slot < qcap) {
+            s_q[2 * slot] = threadIdx.x | (w.pa << 8) | (w.pq << 16) | (w.na << 24);  // all < 256
+            s_q[2 * slot + 1] = w.nq;
+        } else {
+            (void)walk(col, lut, limit, w, ~0u);
+            slot = ~0u;
+        }
     }
     __syncthreads();
-    const uint32_t qn = *s_qn;
+    const uint32_t qn = min(*s_qn, qcap);
     if (threadIdx.x < 64) {
         for (uint32_t i = threadIdx.x; i < qn; i += 64) {
             const uint32_t a = s_q[2 * i];
@@ -901,14 +908,18 @@ __device__ __forceinline__ bool resolve_block(const EgDecParams& P, const uint32
 // DIAG (diagnostic builds, DCT3D_DIAG_FRONT, timing only): 1 = the staging alone, 2 = + the pass-0
 // interior loop, 3 = + the whole pass-0 parse, 4 = + the barrier and the exits in LDS, 5 = + the resolve
 // walk (no stores); nothing is written
+// LDS: table + window + a 60-entry walk queue + 5 words = 23,028 bytes, 7 blocks per CU with 72 VGPRs (the
+// pass is latency-bound: 5 blocks instead of 6 cost it 11 %, profiles/r06/front/r06_socc).  The pass-0
+// exits reach the next thread by a shuffle, across waves through 4 words.
+constexpr uint32_t kSyncQCap = 60;
 template <int DIAG>
 __device__ __forceinline__ void sync_body(const EgDecParams& P, int iteration, int resolve) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + 3 * kEgBlock + 1];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + 2 * kSyncQCap + 1 + kEgWaves];
     uint8_t* const s_lut = (uint8_t*)lds;
     uint32_t* const win = lds + kLutBytes / 4;
-    uint32_t* const s_exit = win + kColBytes / 4;
-    uint32_t* const s_q = s_exit + kEgBlock;  // the resolve's walk queue (resolve_block), its count after it
-    uint32_t* const s_qn = s_q + 2 * kEgBlock;
+    uint32_t* const s_q = win + kColBytes / 4;  // the resolve's walk queue (resolve_block), its count after it
+    uint32_t* const s_qn = s_q + 2 * kSyncQCap;
+    uint32_t* const s_xb = s_qn + 1;  // each wave's last pass-0 exit
     copy_lut(s_lut);
     if (threadIdx.x == 0) *s_qn = 0u;
     const bool rs = iteration == 0 && resolve;
@@ -955,10 +966,12 @@ __device__ __forceinline__ void sync_body(const EgDecParams& P, int iteration, i
         if (iteration > 0 && ex != P.exit_in[t]) atomicOr((unsigned int*)&P.status[0], 1u);
         return;
     }
-    s_exit[threadIdx.x] = invalid ? ~0u : pos;
+    const uint32_t xv = invalid ? ~0u : pos;
+    uint32_t ep = __shfl_up(xv, 1, 64);  // the chunk before's pass-0 exit, in its coordinates
+    if ((threadIdx.x & 63) == 63) s_xb[threadIdx.x >> 6] = xv;
     __syncthreads();
+    if ((threadIdx.x & 63) == 0) ep = threadIdx.x ? s_xb[(threadIdx.x >> 6) - 1] : ~0u;
     const bool own = live && threadIdx.x > 0;  // thread 0: the helper chunk (written by its owner block)
-    const uint32_t ep = threadIdx.x ? s_exit[threadIdx.x - 1] : ~0u;  // in the chunk before's coordinates
     // the true start as pass 0 knows it (chunk 0: its first bit)
     const uint32_t e = t == 0 ? 0u : (ep == ~0u ? ~0u : ep - (uint32_t)kChunkBits);
     if (DIAG == 4) {
@@ -966,7 +979,8 @@ __device__ __forceinline__ void sync_body(const EgDecParams& P, int iteration, i
         return;
     }
     uint32_t x;
-    const bool fail = resolve_block(P, win, s_lut, s_q, s_qn, first, own, e, pos, invalid, stop, limit, b0, n, x);
+    const bool fail = resolve_block(P, win, s_lut, s_q, s_qn, first, own, e, pos, invalid, stop, limit, b0, n, x,
+                                    kSyncQCap);
     if (DIAG == 5) {
         if (fail && n == 0xFFFFFFFFu) P.count[0] = x;
         return;
@@ -977,7 +991,7 @@ __device__ __forceinline__ void sync_body(const EgDecParams& P, int iteration, i
     const uint64_t fb = __ballot(fail);
     if (fb != 0ull && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(fb)) atomicOr((unsigned int*)&P.status[0], 1u);
 }
-__global__ __launch_bounds__(kEgBlock) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
+__global__ __launch_bounds__(kEgBlock, 7) void eg_sync_kernel(EgDecParams P, int iteration, int resolve) {
     sync_body<0>(P, iteration, resolve);
 }
 #ifdef DCT3D_DIAG_FRONT
