@@ -449,7 +449,9 @@ constexpr uint32_t kLutBytes = 1u << 12;
 // The window of chunks first + c, c < kEgBlock (first may be -1: block 0 of the resolving pass), then the
 // caller's barrier.  Thread c loads its chunk's words (four 16-byte loads + three, all in flight at once),
 // funnel-shifts them by the stream's bit offset and writes them down its column.  Words past the stream
-// (or before it: chunk -1) are zero.
+// (or before it: chunk -1) are zero.  PAD: words in front of each column (the mark pass's first mark
+// slots); a group of 32 columns then spans 32 (kColW + PAD) words.
+template <uint32_t PAD = 0>
 __device__ __forceinline__ void stage_columns(const EgDecParams& P, uint32_t* win, int64_t first) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
     const int64_t b0 = (int64_t)P.start_bit + (first + (int64_t)threadIdx.x) * (int64_t)kChunkBits;
@@ -474,7 +476,7 @@ __device__ __forceinline__ void stage_columns(const EgDecParams& P, uint32_t* wi
     }
 #pragma unroll
     for (uint32_t j = 0; j <= kColW; j++) g[j] = __builtin_bswap32(g[j]);
-    uint32_t* col = win + (threadIdx.x >> 5) * (32 * kColW) + (threadIdx.x & 31);
+    uint32_t* col = win + (threadIdx.x >> 5) * (32 * (kColW + PAD)) + 32 * PAD + (threadIdx.x & 31);
     if (o) {
 #pragma unroll
         for (uint32_t j = 0; j < kColW; j++) col[32 * j] = __builtin_amdgcn_alignbit(g[j], g[j + 1], 32u - o);
@@ -483,8 +485,9 @@ __device__ __forceinline__ void stage_columns(const EgDecParams& P, uint32_t* wi
         for (uint32_t j = 0; j < kColW; j++) col[32 * j] = g[j];
     }
 }
-__device__ __forceinline__ const uint32_t* column(const uint32_t* win) {
-    return win + (threadIdx.x >> 5) * (32 * kColW) + (threadIdx.x & 31);
+template <uint32_t PAD = 0, typename W>
+__device__ __forceinline__ W* column(W* win) {
+    return win + (threadIdx.x >> 5) * (32 * (kColW + PAD)) + 32 * PAD + (threadIdx.x & 31);
 }
 
 // chunk-relative form of an absolute bit position (clamped to [0, 2^32 - 1])
@@ -647,13 +650,21 @@ constexpr EgLut<B> make_eg_lut() {
     }
     return t;
 }
-__device__ constexpr EgLut<kEgLutBits> kEgLut = make_eg_lut<kEgLutBits>();
+template <int B>
+__device__ constexpr EgLut<B> kEgLutT = make_eg_lut<B>();
 // the block's copy of the table: 16-byte pieces, ordered by the staging's barrier
+template <int B = kEgLutBits>
 __device__ __forceinline__ void copy_lut(uint8_t* s_lut) {
-    static_assert(kLutBytes % (16 * kEgBlock) == 0, "whole 16-byte pieces per thread");
+    constexpr uint32_t kBytes = 1u << B;
+    if constexpr (kBytes < 16 * kEgBlock) {  // 11 bits: 8 bytes per thread
+        static_assert(kBytes == 8 * kEgBlock, "whole 8-byte pieces per thread");
+        *(uint2*)(s_lut + 8 * threadIdx.x) = *(const uint2*)(kEgLutT<B>.e + 8 * threadIdx.x);
+    } else {
+        static_assert(kBytes % (16 * kEgBlock) == 0, "whole 16-byte pieces per thread");
 #pragma unroll
-    for (uint32_t r = 0; r < kLutBytes / (16 * kEgBlock); r++)
-        *(uint4*)(s_lut + 16 * (threadIdx.x + r * kEgBlock)) = *(const uint4*)(kEgLut.e + 16 * (threadIdx.x + r * kEgBlock));
+        for (uint32_t r = 0; r < kBytes / (16 * kEgBlock); r++)
+            *(uint4*)(s_lut + 16 * (threadIdx.x + r * kEgBlock)) = *(const uint4*)(kEgLutT<B>.e + 16 * (threadIdx.x + r * kEgBlock));
+    }
 }
 static_assert(kEgLutBits <= 15, "counts and widths fit 4 bits");
 
@@ -687,13 +698,14 @@ __device__ __forceinline__ void pos_step_undo(bool bad, uint32_t w_last, uint32_
 // the mark falls on the table's second .. k-th code, whose bit offsets the table does not give; then only
 // the first code (its width by clz).  The mark is then always the run's d0-th value or the first code: bit
 // p0 + d0 of the step.  (Round 5: the table in the mark pass, 430 -> 356 us per c8 step, profiles/r05/mark_lut.)
+template <int B = kEgLutBits>
 __device__ __forceinline__ uint32_t pos_step_lut_mark(const uint32_t* col, const uint8_t* lut, uint32_t& p, bool& bad,
                                                       uint32_t d0, uint32_t& w_last) {
     uint32_t hi, lo;
     col_bits64(col, p, hi, lo);
     const uint32_t n1 = __builtin_clz(~hi | 1u);
     const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
-    const uint32_t e = lut[th >> (32 - kEgLutBits)];
+    const uint32_t e = lut[th >> (32 - B)];
     const uint32_t k = e & 15u;
     const uint32_t zz = ffbh_u32(th);
     // (bitwise, not short-circuit: the compiler made branches of &&)
@@ -730,6 +742,7 @@ __device__ __forceinline__ uint32_t pos_step_lut_bounded(const uint32_t* col, co
     return n1 + (table ? k : (take1 ? 1u : 0u));
 }
 // ... and with the mark pass's one-mark rule (pos_step_lut_mark)
+template <int B = kEgLutBits>
 __device__ __forceinline__ uint32_t pos_step_lut_mark_bounded(const uint32_t* col, const uint8_t* lut, uint32_t& p,
                                                               bool& bad, uint32_t d0, uint32_t stop) {
     const uint32_t room = stop - p;
@@ -737,7 +750,7 @@ __device__ __forceinline__ uint32_t pos_step_lut_mark_bounded(const uint32_t* co
     col_bits64(col, p, hi, lo);
     const uint32_t n1 = __builtin_clz(~hi | (0x80000000u >> min(room, 31u)));
     const uint32_t th = (uint32_t)(((((uint64_t)hi << 32) | lo) << n1) >> 32);
-    const uint32_t e = lut[th >> (32 - kEgLutBits)];
+    const uint32_t e = lut[th >> (32 - B)];
     const uint32_t k = e & 15u, wt = e >> 4;
     const uint32_t zz = ffbh_u32(th);
     const bool has = ((th >> 31) == 0u) & (n1 < room);
@@ -1053,14 +1066,29 @@ __device__ __forceinline__ uint64_t block_lookback(uint64_t* desc, int64_t b, ui
 }
 
 // The mark parse of one chunk from its true start sp (chunk-relative) with its first value idx0: the bit
-// position of every 32nd value.  The marks are collected in the thread's slot myk (2 bytes each, relative
-// to the true start; kMkSlot entries, the last a dummy target for steps without a mark: no branch) and
-// written out at the end, each thread its consecutive marks back to back, so that the L2 assembles whole
+// position of every 32nd value.  The marks are collected in the thread's slots myk[SS * k] (2 bytes each,
+// relative to the true start) and written out at the end, each thread its consecutive marks back to back, so that the L2 assembles whole
 // lines (round 4: WRITE_SIZE 1.67 -> 0.52 GB, the pass 708 -> 529 us; stored one at a time as the parse
 // reached them the lines were written back partial).  Marks leave as the low 16 bits of their bit position
 // (round 5), the whole position of every 64th (a consumer group's first) in mark_base (mark_offset).
-constexpr uint32_t kMkSlot = 17;  // 16 marks (a chunk's true parse takes <= 512 values) + the dummy
-template <bool WRITE = true>
+// Every step of the interior loops stores its mark candidate to the current slot, and a hit moves on to the
+// next (no branch): a step without a mark leaves a value in the slot after the last mark, which the next
+// mark overwrites or nobody reads -- kMkSlot entries: 16 marks (a chunk's true parse takes <= 512 values)
+// and that one.
+// Slot layout (round 6): mark k of a chunk lives in word k - kMkPad of the chunk's own column (SS = 64:
+// 128 bytes per slot, the column's stride), the first kMkPad in words in front of the column.  A column word
+// is dead once the parse has passed it: mark k sits at value >= 32 k of the chunk, so at bit >= 32 k, and
+// slot k is written only after mark k - 1 (bit >= 32 (k - 1)) -- from then on the steps use words >=
+// k - 1 (col_bits64 also reads word p / 32 - 1 at p = 0 mod 32, and ignores it; the checked reader and
+// the undo of a long code never go below the last mark), above word k - kMkPad.  So the pass needs no LDS
+// of its own for the marks: 24.6 instead of 31.3 KB per block, 6 blocks per CU instead of 5.
+constexpr uint32_t kMkSlot = 17;
+constexpr uint32_t kMkPad = 2;
+#ifndef DCT3D_MARK_LUT_BITS  // A/B only: the mark pass's table width
+#define DCT3D_MARK_LUT_BITS 12
+#endif
+constexpr int kMarkLutBits = DCT3D_MARK_LUT_BITS;
+template <bool WRITE = true, uint32_t SS = 1, int LB = kEgLutBits>
 __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t* col, const uint8_t* lut, uint16_t* myk,
                                            int64_t b0, uint32_t sp, uint64_t idx0) {
     const uint32_t end = (uint32_t)kChunkBits;
@@ -1074,7 +1102,6 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
     const uint32_t ph = (uint32_t)idx0 & (kMarkVals - 1);
     const uint32_t sh = ph ? 1u : 0u;       // slot of value j: (ph + j) / 32 - sh (16 slots)
     const uint64_t gm0 = idx0 / kMarkVals;  // mark gm0 + k = mark of value idx0 + 32 k - ph
-    uint16_t* const dummy = myk + (kMkSlot - 1);
     uint32_t i = 0, code;
     // Interior of the chunk: a step moves at most 31 + 31 bits and 32 values, so while the parse is
     // kLeanMargin bits short of the chunk end and of the data limit none of the bounds below can bind -- a
@@ -1093,9 +1120,9 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
         uint16_t* mp = myk;
         auto mark = [&](uint32_t at, uint32_t nv, uint32_t d0) {
             const bool hit = d0 < nv;
-            *(hit ? mp : dummy) = (uint16_t)(at - sp);  // no branch
+            *mp = (uint16_t)(at - sp);  // no branch: a miss is overwritten by the next mark or never read
             nm += hit ? kMarkVals : 0u;
-            mp += hit ? 1 : 0;
+            mp += hit ? SS : 0u;
             i += nv;
         };
         // table steps that stop on the mark (nv <= 32): the mark is value d0 of the step, at bit p0 + d0
@@ -1103,7 +1130,7 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
         while (!bad & (p < fast_end)) {
             const uint32_t p0 = p;
             const uint32_t d0 = nm - i;
-            mark(p0 + d0, pos_step_lut_mark(col, lut, p, bad, d0, w_last), d0);
+            mark(p0 + d0, pos_step_lut_mark<LB>(col, lut, p, bad, d0, w_last), d0);
         }
         // the long or invalid code the last step met (its mark, if it is one, was stored at its first bit:
         // the checked loop stores the same or ends the pass)
@@ -1114,7 +1141,7 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
         while (!bad & (p < bend)) {
             const uint32_t p0 = p;
             const uint32_t d0 = nm - i;
-            mark(p0 + d0, pos_step_lut_mark_bounded(col, lut, p, bad, d0, bend), d0);
+            mark(p0 + d0, pos_step_lut_mark_bounded<LB>(col, lut, p, bad, d0, bend), d0);
         }
     }
     if (i < rem && p < end) {
@@ -1131,7 +1158,7 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
             const uint32_t k = r.ones(min(room, 64u));
             if (k) {  // values i .. i + k - 1 are zeros at bits p0 .. p0 + k - 1
                 for (uint32_t j = ((ph + i + kMarkVals - 1) & ~(kMarkVals - 1)) - ph; j < i + k; j += kMarkVals)
-                    myk[(ph + j) / kMarkVals - sh] = (uint16_t)(p0 + (j - i) - sp);
+                    myk[SS * ((ph + j) / kMarkVals - sh)] = (uint16_t)(p0 + (j - i) - sp);
                 i += k;
                 if (ends_here && i == rem) P.status[1] = (uint64_t)b0 + r.pos;  // the bit after the last wanted value
             }
@@ -1147,7 +1174,7 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
             // Every code of the wanted values is parsed here or in the lean loops above, which leave every
             // such code to this loop.
             if (code >= 0x10000u) atomicOr((unsigned int*)&P.status[3], 1u);
-            if (((ph + i) & (kMarkVals - 1)) == 0) myk[(ph + i) / kMarkVals - sh] = (uint16_t)(p1 - sp);
+            if (((ph + i) & (kMarkVals - 1)) == 0) myk[SS * ((ph + i) / kMarkVals - sh)] = (uint16_t)(p1 - sp);
             if (++i == rem && ends_here) P.status[1] = (uint64_t)b0 + r.pos;
         }
     }
@@ -1159,7 +1186,7 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
     const uint64_t a0 = (uint64_t)b0 + sp;
     uint16_t* const mk = P.mark + gm0;
     for (uint32_t k = sh; k < (ph + i + kMarkVals - 1) / kMarkVals; k++) {
-        const uint64_t m = a0 + myk[k - sh];
+        const uint64_t m = a0 + myk[SS * (k - sh)];
         mk[k] = (uint16_t)m;
         if (((gm0 + k) & (kMarkGroup - 1)) == 0) P.mark_base[(gm0 + k) / kMarkGroup] = m;
     }
@@ -1169,12 +1196,13 @@ __device__ __forceinline__ void mark_chunk(const EgDecParams& P, const uint32_t*
 // exit of the chunk before), its first value index from the scan.
 template <int DIAG>
 __device__ __forceinline__ void mark_body(const EgDecParams& P) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[(kLutBytes + kColBytes) / 4 + kEgBlock * kMkSlot / 2 + 1 + 6];
+    constexpr uint32_t kWinWords = kEgBlock * (kColW + kMkPad);  // the columns with the marks' pad
+    constexpr uint32_t kMLut = 1u << kMarkLutBits;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kMLut / 4 + kWinWords + kEgWaves + 1];
     uint8_t* const s_lut = (uint8_t*)lds;
-    uint32_t* const win = lds + kLutBytes / 4;
-    uint16_t* const s_mk = (uint16_t*)(win + kColBytes / 4);
-    uint32_t* const s_ws = (uint32_t*)(s_mk + kEgBlock * kMkSlot) + 1;  // the waves' count sums, then the base
-    copy_lut(s_lut);
+    uint32_t* const win = lds + kMLut / 4;
+    uint32_t* const s_ws = win + kWinWords;  // the waves' count sums, then the parts' sum
+    copy_lut<kMarkLutBits>(s_lut);
     // the sync pass's verdict: status[0] != 0 only after a speculative pass 0 whose chunks did not all
     // resolve (the converged confirming passes leave it 0): no marks, the consumers skip themselves
     if (P.status[0] != 0) {  // grid-uniform
@@ -1193,7 +1221,7 @@ __device__ __forceinline__ void mark_body(const EgDecParams& P) {
     const uint32_t pv = (wave == 0 && lane < pj) ? P.part[(uint64_t)blockIdx.x - pj + lane] : 0u;
     const uint64_t bb = P.bsum[blockIdx.x >> 4];
     __builtin_amdgcn_s_setprio(0);
-    stage_columns(P, win, first);
+    stage_columns<kMkPad>(P, win, first);
     // the block's exclusive scan of the counts: in the wave by shuffles, across the waves through LDS
     uint32_t incl = cnt;
 #pragma unroll
@@ -1210,7 +1238,7 @@ __device__ __forceinline__ void mark_body(const EgDecParams& P) {
     }
     __syncthreads();
     if (DIAG == 1) {
-        if (column(win)[0] == 0x12345678u && P.n_chunks == 0) P.count[0] = 1u;  // keeps the staging
+        if (column<kMkPad>(win)[0] == 0x12345678u && P.n_chunks == 0) P.count[0] = 1u;  // keeps the staging
         return;
     }
     if (t >= P.n_chunks) return;
@@ -1222,7 +1250,8 @@ __device__ __forceinline__ void mark_body(const EgDecParams& P) {
     if (idx0 >= P.n_values) return;
     if (s == kNoExit) return;  // the true parse stopped in an earlier chunk: reported by that chunk
     const int64_t b0 = (int64_t)P.start_bit + (int64_t)t * (int64_t)kChunkBits;
-    mark_chunk<DIAG == 0>(P, column(win), s_lut, s_mk + threadIdx.x * kMkSlot, b0, rel_bit(s, b0), idx0);
+    uint32_t* const col = column<kMkPad>(win);
+    mark_chunk<DIAG == 0, 64, kMarkLutBits>(P, col, s_lut, (uint16_t*)(col - 32 * kMkPad), b0, rel_bit(s, b0), idx0);
 }
 __global__ __launch_bounds__(kEgBlock) void eg_mark_kernel(EgDecParams P) { mark_body<0>(P); }
 #ifdef DCT3D_DIAG_FRONT
