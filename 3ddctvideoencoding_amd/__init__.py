@@ -385,7 +385,8 @@ class Context:
     def decode_eg_dev(self, d_bytes, nbytes: int, start_bit: int, width: int, height: int, n_stacks: int,
                       d_frames) -> int:
         """Fused device path: Exp-Golomb stream (device, 4-byte aligned) -> u8 frames (device), no int32
-        intermediate; returns the bit after the last value."""
+        intermediate; returns the bit after the last value once the stream's verdict is known -- the frames
+        complete asynchronously on the context stream (as decode_stacks_dev; synchronize() or stream order)."""
         eb = C.c_uint64(0)
         _check(lib().dct3d_decode_eg_dev(self._h, _tptr(d_bytes), nbytes, start_bit, width, height, n_stacks,
                                          _tptr(d_frames), C.byref(eb)), "dct3d_decode_eg_dev")

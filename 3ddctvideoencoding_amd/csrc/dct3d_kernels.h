@@ -130,8 +130,10 @@ struct EgDecParams {
     uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output
     // (decode_eg_kernel, optional) the host's pinned copy of status[0..5], written by block 0 as it starts
-    // (every word is final by then): the call's verdict needs no copy kernel behind the consumer
+    // (every word is final by then), then [6] = seq (system-scope release): the host polls for seq and
+    // returns while the consumer still runs (the raster completes on the stream, as every *_dev output)
     uint64_t* status_host;
+    uint64_t seq;
     // (decode_eg_kernel, optional) the ctx's other status slot, zeroed by block 0 for the next call (whose
     // front then needs no memset)
     uint64_t* status_clear;

@@ -465,7 +465,9 @@ def main():
         else:  # fused (dct3d_decode_eg_dev): stream -> raster, no int32 intermediate; the step is the whole
             # EG stage, so no per-step events (their packets and the host work would sit in the timed region)
             def step():
-                ctx.decode_eg_dev(eg_stream, nbytes, 0, width, height, stacks, out)  # synchronises
+                # returns with the verdict, the raster completing on the stream (the timed region ends with a
+                # device synchronisation)
+                ctx.decode_eg_dev(eg_stream, nbytes, 0, width, height, stacks, out)
     elif direction == "encode_eg" and a.eg_two_step:
         eg_cap = n_cubes * cs  # 8 bits per value: far above what quantised content needs
         eg_out = torch.empty(eg_cap // 4, dtype=torch.int32, device="cuda")

@@ -231,8 +231,10 @@ int dct3d_eg_decode_dev(dct3d_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes,
 /* Device stream in, device raster out, fused: decoder.c:209-295 after the inflate
  * for n_stacks stacks -- Exp-Golomb decode, reorder, dequantisation, IDCT, clamp/truncate -- without the
  * int32 cube-major intermediate: the decode kernel parses each of its cubes from the stream directly.
- * Stream arguments, *end_bit and errors as dct3d_eg_decode_dev; the raster as dct3d_decode_stacks_dev.
- * Synchronises the context stream. */
+ * Stream arguments, *end_bit and errors as dct3d_eg_decode_dev; the raster as dct3d_decode_stacks_dev:
+ * the call returns once *end_bit and the verdict are known (the decode kernel hands them to the host as
+ * it starts), and the raster completes asynchronously on the context stream (use dct3d_synchronize, or
+ * read it in stream order). */
 int dct3d_decode_eg_dev(dct3d_ctx *ctx, const uint8_t *d_bytes, uint64_t nbytes, uint64_t start_bit, int width,
                         int height, int n_stacks, uint8_t *d_raster, uint64_t *end_bit);
 

@@ -207,6 +207,34 @@ def test_fused_decode_1080p_matches_two_step(pkg, gpu_ctx8, gpu_ctx4, depth, kin
     assert np.array_equal(got, ref)
 
 
+@pytest.mark.parametrize("own_stream", [True, False])
+def test_fused_decode_back_to_back(pkg, gpu_ctx8, own_stream):
+    """dct3d_decode_eg_dev returns once the verdict is known, with the consumer still running on the
+    stream: calls queued back to back (no synchronisation between them, alternating contents and
+    outputs, the last call again into the first output) each land their own raster -- on the context's own
+    stream and on a framework stream shared through set_stream"""
+    import torch
+    fr = [pkg.synthetic.frames(1920, 1080, 2 * 8, kind=k, frame0=f) for k, f in (("ramp", 3), ("uniform", 9))]
+    enc = [gpu_ctx8.encode_eg(x) for x in fr]
+    refs = [_decode_two_step(gpu_ctx8, d, 1920, 1080, 2)[0] for d, _ in enc]
+    ctx = pkg.Context(0, 8, 8, 8)
+    try:
+        st = None if own_stream else torch.cuda.Stream()
+        if st is not None:
+            ctx.set_stream(st.cuda_stream)
+        ds = [_stream_dev(d) for d, _ in enc]
+        outs = [torch.empty((16, 1080, 1920), dtype=torch.uint8, device="cuda") for _ in range(3)]
+        torch.cuda.synchronize()
+        order = [(0, 0), (1, 1), (0, 2), (1, 0)]  # (content, output): output 0 is written twice
+        with torch.cuda.stream(st) if st is not None else torch.cuda.stream(torch.cuda.current_stream()):
+            for k, o in order:
+                assert ctx.decode_eg_dev(ds[k], len(enc[k][0]), 0, 1920, 1080, 2, outs[o]) == enc[k][1]
+            got = [x.cpu().numpy() for x in outs]  # on the decode's stream (st) or the legacy default one
+        assert np.array_equal(got[0], refs[1]) and np.array_equal(got[1], refs[1]) and np.array_equal(got[2], refs[0])
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("kind", ["ramp", "uniform", "checker", "full"])
 def test_fused_decode_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, kind):
