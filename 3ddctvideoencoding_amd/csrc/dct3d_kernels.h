@@ -97,6 +97,19 @@ struct EgParams {
     uint64_t* status_clear;
 };
 
+// A call's verdict as one 64-bit word (hand-off to the host while the call's last kernels still run): the
+// call's sequence number (low 16 bits) in bits 63..48, flags in 47..40, a value < 2^40 in 39..0 (flag 0x80:
+// the value did not fit -- the host then waits for the stream and reads the whole words).  One store, so
+// the host never sees part of it, and no ordering against other stores is needed: the device writes it
+// with a system-scope relaxed store (written through; a release would write back the whole L2 first,
+// measured no faster).
+constexpr uint64_t kTagValueMask = (1ull << 40) - 1;
+constexpr uint32_t kTagOverflow = 0x80;
+__host__ __device__ inline uint64_t hand_off_tag(uint64_t seq, uint64_t value, uint32_t flags) {
+    if (value > kTagValueMask) flags |= kTagOverflow;
+    return ((seq & 0xFFFFull) << 48) | ((uint64_t)(flags & 0xFF) << 40) | (value & kTagValueMask);
+}
+
 // Exp-Golomb decode (self-synchronising chunks, see dct3d_eg.hip)
 constexpr uint64_t kEgChunkBits = 512;  // bits per parse chunk (one thread each)
 // Marks (the bit position of every 32nd value) are stored as their low 16 bits; the whole position of a
@@ -130,8 +143,9 @@ struct EgDecParams {
     uint64_t* mark_base;       // [n_values / 32 / kMarkGroup + 1] bit position of every kMarkGroup-th mark
     int32_t* q;                // cube-major output
     // (decode_eg_kernel, optional) the host's pinned copy of status[0..5], written by block 0 as it starts
-    // (every word is final by then), then [6] = seq (system-scope release): the host polls for seq and
-    // returns while the consumer still runs (the raster completes on the stream, as every *_dev output)
+    // (every word is final by then), and [6] = hand_off_tag(seq, end bit, verdict flags): the host polls
+    // for it and returns while the consumer still runs (the raster completes on the stream, as every *_dev
+    // output)
     uint64_t* status_host;
     uint64_t seq;
     // (decode_eg_kernel, optional) the ctx's other status slot, zeroed by block 0 for the next call (whose

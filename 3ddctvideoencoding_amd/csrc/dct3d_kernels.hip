@@ -525,10 +525,12 @@ __global__ __launch_bounds__(kBlock, 4) void decode_eg_kernel(DecodeParams P, Eg
     constexpr uint32_t SOFF = 40;
     __shared__ __attribute__((aligned(16))) uint16_t s_soff[PARTS * SOFF];
     dec_clear_next_slot(P);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && E.status_host) {  // the verdict to the host, then its sequence number
+    if (blockIdx.x == 0 && threadIdx.x == 0 && E.status_host) {  // the verdict to the host: the words, the tag
+        uint64_t w[6];
 #pragma unroll
-        for (int i = 0; i < 6; i++) E.status_host[i] = E.status[i];
-        __hip_atomic_store(E.status_host + 6, E.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int i = 0; i < 6; i++) E.status_host[i] = w[i] = E.status[i];
+        const uint32_t fl = (uint32_t)(w[2] & 7u) | (w[4] < E.n_values ? 8u : 0u);  // flags, short by the scan
+        __hip_atomic_store(E.status_host + 6, hand_off_tag(E.seq, w[1], fl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (blockIdx.x == 0 && threadIdx.x < 6 && E.status_clear) E.status_clear[threadIdx.x] = 0u;
     // corrupt / short / empty stream: reported by the mark pass (block-uniform)

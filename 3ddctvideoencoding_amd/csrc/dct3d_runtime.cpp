@@ -941,6 +941,9 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     G.bsum = (uint64_t*)c->d_eg_bsum.p;
     G.status = sw;
     eg_status_handoff(c, G);  // the stitch kernel (the last of launch_eg_compact) hands the words over
+    // (Round 6: handed over by the compaction's block 0 instead, the call returning while the compaction and
+    // the stitch ran, the compaction slowed 151 -> 205 us beside the next call's launches: c7 +15-25 us per
+    // call, profiles/r06/gaps/async7.  The stream decode's consumer, compute-bound, does not slow.)
     G.head = (uint32_t*)c->d_eg_ht.p;
     G.tail = (uint32_t*)c->d_eg_ht.p + n_seg;
     G.out = (uint32_t*)d_out;
@@ -1116,25 +1119,46 @@ static int eg_decode_front(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes
 // while the consumer still runs -- the raster completes on the context stream, as every *_dev output does,
 // and the caller's next call is queued behind it (round 6: the synchronous return left ~50 us per call with
 // the device idle between the consumer's end and the next call's first kernel, profiles/r06/gaps/).
-static int egd_wait_verdict(dct3d_ctx* c, uint64_t seq, uint64_t* w) {
+// polls the pinned word h_status[word] for the call's hand-off tag (hand_off_tag: its sequence number in the
+// top 16 bits) and returns the tag's value and flags
+static int wait_tag(dct3d_ctx* c, int word, uint64_t seq, uint64_t* value, uint32_t* flags) {
     const volatile uint64_t* h = c->h_status;
+    uint64_t t = 0;
     for (uint32_t n = 1;; n++) {
-        if (h[6] == seq) break;
+        t = h[word];
+        if ((t >> 48) == (seq & 0xFFFFu)) break;
         if ((n & 255u) == 0u) {  // now and then: has the stream ended (or failed) without the hand-off?
             const hipError_t e = hipStreamQuery(c->stream);
             if (e != hipSuccess && e != hipErrorNotReady) return DCT3D_EDEVICE;
-            if (e == hipSuccess && h[6] != seq) return DCT3D_EDEVICE;
+            if (e == hipSuccess && (h[word] >> 48) != (seq & 0xFFFFu)) return DCT3D_EDEVICE;
         }
         __builtin_ia32_pause();
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);
-    for (int i = 0; i < 6; i++) w[i] = h[i];
+    t = h[word];
+    *value = t & kTagValueMask;
+    *flags = (uint32_t)(t >> 40) & 0xFFu;
+    return DCT3D_OK;
+}
+// the decode's verdict from the tag: w[1] = end bit, w[2] = flags, w[4] = a total that passes the short
+// check (the tag's flag 8 says short); the whole words after the stream when the end bit did not fit
+static int egd_wait_verdict(dct3d_ctx* c, const EgDecParams& D, uint64_t* w) {
+    uint64_t v = 0;
+    uint32_t fl = 0;
+    if (wait_tag(c, 6, D.seq, &v, &fl)) return DCT3D_EDEVICE;
+    if (fl & kTagOverflow) {
+        if (stream_wait(c)) return DCT3D_EDEVICE;
+        memcpy(w, c->h_status, kEgdStatusBytes);
+        return DCT3D_OK;
+    }
+    w[1] = v;
+    w[2] = fl & 7u;
+    w[4] = (fl & 8u) ? 0u : D.n_values;
     return DCT3D_OK;
 }
 static int eg_decode_status(dct3d_ctx* c, const EgDecParams& D, uint64_t* end_bit) {
     uint64_t w[6] = {0, 0, 0, 0, 0, 0};
     if (D.status_host) {
-        if (egd_wait_verdict(c, D.seq, w)) return DCT3D_EDEVICE;
+        if (egd_wait_verdict(c, D, w)) return DCT3D_EDEVICE;
     } else if (read_status(c, D.status, kEgdStatusBytes, w)) {
         return DCT3D_EDEVICE;
     }

@@ -208,6 +208,33 @@ def test_fused_decode_1080p_matches_two_step(pkg, gpu_ctx8, gpu_ctx4, depth, kin
 
 
 @pytest.mark.parametrize("own_stream", [True, False])
+def test_fused_encode_back_to_back(pkg, gpu_ctx8, own_stream):
+    """dct3d_encode_eg_dev returns once the total is known, the compaction and the stitch still running:
+    calls queued back to back (alternating contents and outputs, the last call again into the first
+    output) each land their own stream, on the context's own stream and on a shared framework stream"""
+    import torch
+    fr = [pkg.synthetic.frames(1920, 1080, 2 * 8, kind=k, frame0=f) for k, f in (("ramp", 4), ("uniform", 8))]
+    refs = [gpu_ctx8.encode_eg(x) for x in fr]
+    ctx = pkg.Context(0, 8, 8, 8)
+    try:
+        st = None if own_stream else torch.cuda.Stream()
+        if st is not None:
+            ctx.set_stream(st.cuda_stream)
+        ds = [torch.from_numpy(x).cuda() for x in fr]
+        cap = fr[0].size * 2
+        outs = [torch.zeros(cap // 4, dtype=torch.int32, device="cuda") for _ in range(3)]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st) if st is not None else torch.cuda.stream(torch.cuda.current_stream()):
+            for k, o in [(0, 0), (1, 1), (0, 2), (1, 0)]:
+                assert ctx.encode_eg_dev(ds[k], 1920, 1080, 2, outs[o], cap) == refs[k][1]
+            got = [x.cpu().numpy().view(np.uint8) for x in outs]
+        for o, k in ((0, 1), (1, 1), (2, 0)):
+            assert got[o][: len(refs[k][0])].tobytes() == refs[k][0]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("own_stream", [True, False])
 def test_fused_decode_back_to_back(pkg, gpu_ctx8, own_stream):
     """dct3d_decode_eg_dev returns once the verdict is known, with the consumer still running on the
     stream: calls queued back to back (no synchronisation between them, alternating contents and
