@@ -262,6 +262,26 @@ def test_fused_decode_back_to_back(pkg, gpu_ctx8, own_stream):
         ctx.close()
 
 
+def test_fused_decode_queue_stress(pkg, gpu_ctx8):
+    """Many calls queued behind running consumers (the host runs a call ahead of the device): two different
+    1080p streams of 16 stacks alternate over 12 calls into 12 outputs -- each call's scan, marks and
+    consumer must see only its own stream's values (stale values of the other stream would decode to
+    garbage)"""
+    import torch
+    fr = [pkg.synthetic.frames(1920, 1080, 16 * 8, kind=k, frame0=f) for k, f in (("ramp", 2), ("uniform", 6))]
+    enc = [gpu_ctx8.encode_eg(x) for x in fr]
+    refs = [_decode_two_step(gpu_ctx8, d, 1920, 1080, 16)[0] for d, _ in enc]
+    ds = [_stream_dev(d) for d, _ in enc]
+    outs = [torch.empty((128, 1080, 1920), dtype=torch.uint8, device="cuda") for _ in range(12)]
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        k = i % 2
+        assert gpu_ctx8.decode_eg_dev(ds[k], len(enc[k][0]), 0, 1920, 1080, 16, o) == enc[k][1]
+    gpu_ctx8.synchronize()
+    for i, o in enumerate(outs):
+        assert np.array_equal(o.cpu().numpy(), refs[i % 2]), f"call {i}"
+
+
 @pytest.mark.parametrize("depth", [8, 4])
 @pytest.mark.parametrize("kind", ["ramp", "uniform", "checker", "full"])
 def test_fused_decode_matches_oracle(pkg, oracle, plan8, plan4, gpu_ctx8, gpu_ctx4, depth, kind):
