@@ -319,6 +319,9 @@ __global__ __launch_bounds__(kEgBlock) void eg_stitch_kernel(EgParams P) {
         if (P.status_host) P.status_host[threadIdx.x] = P.status[threadIdx.x];
         if (P.status_clear) P.status_clear[threadIdx.x] = 0u;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && P.status_host && P.seq)  // the verdict as one tag word
+        __hip_atomic_store(P.status_host + 7, hand_off_tag(P.seq, P.status[0], (uint32_t)(P.status[1] & 3u)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (P.status[1] != 0) return;
     const uint64_t g = (uint64_t)blockIdx.x * kEgBlock + threadIdx.x;
     if (g >= P.n_cubes) return;

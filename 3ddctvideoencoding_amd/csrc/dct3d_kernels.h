@@ -95,6 +95,7 @@ struct EgParams {
     // of the ctx's two status slots, zeroed for the next call (no copy kernel and no memset per call)
     uint64_t* status_host;
     uint64_t* status_clear;
+    uint64_t seq;  // (with status_host) the call's tag: [7] = hand_off_tag(seq, total bits, flags), polled by the host
 };
 
 // A call's verdict as one 64-bit word (hand-off to the host while the call's last kernels still run): the

@@ -107,6 +107,7 @@ struct dct3d_ctx {
     uint64_t* h_status = nullptr;
     uint64_t* h_status_dev = nullptr;  // its device-side address (decode_eg_kernel writes the words there)
     uint64_t egd_seq = 0;              // stream-decode calls so far: decode_eg_kernel's hand-off tag (h_status[6])
+    uint64_t eg_seq = 0;               // stream-encode calls so far: eg_stitch_kernel's hand-off tag (h_status[7])
     // host-pointer pipeline: copy streams, slot events, double-buffered slots
     hipStream_t s_up = nullptr, s_down = nullptr;
     hipEvent_t pe_in[2] = {}, pe_done[2] = {};
@@ -192,14 +193,26 @@ static uint64_t* eg_status_begin(dct3d_ctx* c, int* rc) {
 static void eg_status_handoff(dct3d_ctx* c, EgParams& P) {
     P.status_host = c->h_status_dev;
     P.status_clear = (uint64_t*)c->d_eg_status.p + 2 * (c->eg_slot ^ 1);
+    P.seq = ++c->eg_seq;
 }
-// after the stitch kernel was enqueued with the hand-off: its words in the pinned buffer
-static int eg_status_end(dct3d_ctx* c, bool handoff, const uint64_t* st, uint64_t* out) {
+static int wait_tag(dct3d_ctx* c, int word, uint64_t seq, uint64_t* value, uint32_t* flags);
+// after the stitch kernel was enqueued with the hand-off: the call returns when the stitch's block 0 has
+// handed the verdict over (the tag), the stitch's last words completing on the stream (a wait for the
+// stream's end instead took ~30 us longer to return, profiles/r06/gaps/timed)
+static int eg_status_end(dct3d_ctx* c, bool handoff, const uint64_t* st, uint64_t* out, uint64_t seq = 0) {
     int rc;
     if (handoff) {
         c->eg_clean[c->eg_slot ^ 1] = true;
-        rc = stream_wait(c);
-        if (!rc) memcpy(out, c->h_status, 16);
+        uint64_t v = 0;
+        uint32_t fl = 0;
+        rc = wait_tag(c, 7, seq, &v, &fl);
+        if (!rc && (fl & kTagOverflow)) {  // the total did not fit the tag: the words, after the stream
+            rc = stream_wait(c);
+            if (!rc) memcpy(out, c->h_status, 16);
+        } else if (!rc) {
+            out[0] = v;
+            out[1] = fl & 3u;
+        }
     } else {
         rc = read_status(c, st, 16, out);
     }
@@ -859,7 +872,7 @@ static int eg_run(dct3d_ctx* c, const int32_t* d_q, uint64_t n_cubes, uint8_t ca
     P.carry_byte = carry_byte;
     if (launch_eg_encode(c->bd, P, c->stream)) return DCT3D_EKERNEL;
     uint64_t st[2] = {0, 0};
-    if (eg_status_end(c, true, sw, st)) return DCT3D_EDEVICE;
+    if (eg_status_end(c, true, sw, st, P.seq)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     if (st[1] & 2) return DCT3D_EINVAL;
     if (st[1] & 1) return DCT3D_ENOSPC;
@@ -958,7 +971,7 @@ int dct3d_encode_eg_dev(dct3d_ctx* c, const uint8_t* d_raster, int w, int h, int
     if (ev) (void)hipEventRecord(ev[2], c->stream);
     if (launch_eg_compact(G, E.slot, seg_cap, c->stream)) return DCT3D_EKERNEL;
     if (ev) (void)hipEventRecord(ev[3], c->stream);
-    if (eg_status_end(c, true, sw, st)) return DCT3D_EDEVICE;
+    if (eg_status_end(c, true, sw, st, G.seq)) return DCT3D_EDEVICE;
     if (total_bits) *total_bits = st[0];
     c->last_units = n_cubes * (uint64_t)c->plan.cs;
     if (st[1] & 1) return DCT3D_ENOSPC;

@@ -191,7 +191,8 @@ int dct3d_inverse_f32_dev(dct3d_ctx *ctx, const float *d_coeffs, size_t n_cubes,
  * i.e. the stream bytes followed by zero padding; *total_bits = carry_bits + the bits written.
  * Values must satisfy |v| < 2^30 (quantised 8-bit content stays below 2^13), else DCT3D_EINVAL.
  * DCT3D_ENOSPC when out_cap is too small (*total_bits is still set; d_out is untouched).
- * Synchronises the context stream (the total is read back). */
+ * Returns once *total_bits is known (the last kernel, eg_stitch_kernel, hands it to the host as it
+ * starts); the last words of d_out complete on the context stream (dct3d_synchronize, or stream order). */
 int dct3d_eg_encode_dev(dct3d_ctx *ctx, const int32_t *d_q, uint64_t n_cubes, uint8_t carry_byte, int carry_bits,
                         uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
 
@@ -207,7 +208,8 @@ int dct3d_encode_eg(dct3d_ctx *ctx, const uint8_t *raster, int width, int height
  * transform kernel, and each wave codes its 8 cubes straight into the stream.  The stream format,
  * carry, d_out and *total_bits are those of dct3d_eg_encode_dev (the bytes are identical to
  * dct3d_encode_stacks_dev followed by dct3d_eg_encode_dev).  DCT3D_ENOSPC when out_cap is too small
- * (*total_bits is still set; d_out is untouched).  Synchronises the context stream. */
+ * (*total_bits is still set; d_out is untouched).  Returns as dct3d_eg_encode_dev: once *total_bits is
+ * known, the last words completing on the context stream. */
 int dct3d_encode_eg_dev(dct3d_ctx *ctx, const uint8_t *d_raster, int width, int height, int n_stacks,
                         uint8_t carry_byte, int carry_bits, uint8_t *d_out, uint64_t out_cap, uint64_t *total_bits);
 
