@@ -167,6 +167,18 @@ __device__ __forceinline__ void eg_lane_emit(const EgFusedParams& E, const uint3
     if (lane == 63) E.seg_bits[wid] = incl;
 }
 
+// Byte offset of cube-major code k (k = (kz*8 + ky)*8 + kx) in K1's staging of one cube.  8x8x8: the rows
+// of face kz are rotated by kz (row ky at slot (ky + kz) mod 8), so that the 16-byte row stores of a
+// ds_write_b128 lane group -- one cube's 8 faces, the same ky -- land on 8 different 4-bank groups (round 6:
+// unrotated, all 8 sat on one: 7 extra LDS cycles per group, 56 per store instruction, most of K1's
+// SQ_LDS_BANK_CONFLICT); the emission's scattered reads are unchanged on average (3.25 -> 3.31 extra cycles
+// per read, tools/k1_lds_sim.py).
+template <int D>
+__device__ __forceinline__ uint32_t k1_code_off(uint32_t k) {
+    if constexpr (D == 8) return (k >> 6) * 128u + ((((k >> 3) + (k >> 6)) & 7u) << 4) + (k & 7u) * 2u;
+    else return (k >> 6) * 128u + (k & 63u) * 2u;
+}
+
 template <int D>
 __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, EgFusedParams E) {
     constexpr int CS = 64 * D;
@@ -177,6 +189,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     // at c * CUBE_B.  8x8x8: cubes 1,056 B apart (a host search over the strides within the wave's region: the
     // emission's scattered 16-bit reads 2.9 -> 2.6 LDS cycles; before: 1,040); 8x8x4: 528 B
     constexpr int FACE = 128;
+    static_assert(FACE == 128, "k1_code_off's face stride");
     constexpr int CUBE_B = (D == 8) ? 1056 : 2 * CS + 16;
     static_assert(8 * CUBE_B <= enc_wave_lds<D>(), "int16 staging must fit the wave region");
     __shared__ __attribute__((aligned(16))) char lds[kWavesPerBlock * enc_wave_lds<D>()];
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
 #pragma unroll
         for (int r = 0; r < CS / kBlock; r++) t[r] = E.diag[threadIdx.x + r * kBlock];
 #pragma unroll
-        for (int r = 0; r < CS / kBlock; r++) s_pos[threadIdx.x + r * kBlock] = (uint16_t)((t[r] >> 6) * FACE + (t[r] & 63) * 2);
+        for (int r = 0; r < CS / kBlock; r++) s_pos[threadIdx.x + r * kBlock] = (uint16_t)k1_code_off<D>(t[r]);
     }
     __syncthreads();
     if (cube0 >= P.n_cubes) return;  // wave-uniform, after the barrier
@@ -265,7 +278,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
     // stage the cubes' Exp-Golomb codes as uint16, cube-major (k = (kz*8 + ky)*8 + kx at byte 2k of cube c)
 #pragma unroll
     for (int ky = 0; ky < 8; ky++) {
-        char* row = wl + c * CUBE_B + kz * FACE + 2 * (ky * 8 + kx0);
+        char* row = wl + c * CUBE_B + kz * FACE + ((D == 8) ? (((ky + kz) & 7) << 4) : 2 * (ky * 8 + kx0));
         if constexpr (D == 8) {
             *(uint4*)row = make_uint4(eg_code_pair(qv[ky][1], qv[ky][0]), eg_code_pair(qv[ky][3], qv[ky][2]),
                                       eg_code_pair(qv[ky][5], qv[ky][4]), eg_code_pair(qv[ky][7], qv[ky][6]));
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(kBlock, 4) void encode_eg_kernel(EncodeParams P, Eg
             const int skz = (D == 8) ? sj : (sj >> 1), skx0 = (D == 8) ? 0 : (sj & 1) * 4;
             const uint32_t k = (uint32_t)((skz * 8 + bit / NB) * 8 + skx0 + bit % NB);
             const int q = exact_coef<D>(R, cube0 + sc, k, lane, (int*)rs, (double*)(rs + kMaxGroupsDev * 4));
-            if (lane == 0) *(uint16_t*)(wl + sc * CUBE_B + (k >> 6) * FACE + (k & 63) * 2) = (uint16_t)(q > 0 ? 2 * q : 1 - 2 * q);
+            if (lane == 0) *(uint16_t*)(wl + sc * CUBE_B + k1_code_off<D>(k)) = (uint16_t)(q > 0 ? 2 * q : 1 - 2 * q);
             if (lane == src) {
                 if (fm_lo) fm_lo &= fm_lo - 1;
                 else fm_hi &= fm_hi - 1;
