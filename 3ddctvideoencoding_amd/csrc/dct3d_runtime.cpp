@@ -1145,7 +1145,9 @@ static int wait_tag(dct3d_ctx* c, int word, uint64_t seq, uint64_t* value, uint3
             if (e != hipSuccess && e != hipErrorNotReady) return DCT3D_EDEVICE;
             if (e == hipSuccess && (h[word] >> 48) != (seq & 0xFFFFu)) return DCT3D_EDEVICE;
         }
-        __builtin_ia32_pause();
+        // a long call (a large stream, a busy device): after ~64 k polls the host thread yields its core
+        if (n < 65536u) __builtin_ia32_pause();
+        else std::this_thread::yield();
     }
     t = h[word];
     *value = t & kTagValueMask;
