@@ -1195,7 +1195,7 @@ int dct3d_eg_decode_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (n_cubes == 0) return DCT3D_OK;
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
     for (int spec = 1;; spec = 0) {
-        EgDecParams D;
+        EgDecParams D{};
         int rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, D, spec && !c->opt_eg_no_resolve);
         if (rc) return rc;
         D.q = d_q;
@@ -1276,7 +1276,7 @@ int dct3d_decode_eg_dev(dct3d_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, u
     if (n_cubes == 0) return DCT3D_OK;
     if (start_bit >= nbytes * 8) return DCT3D_ENODATA;
     for (int spec = 1;; spec = 0) {
-        EgDecParams E;
+        EgDecParams E{};
         if ((rc = eg_decode_front(c, d_bytes, nbytes, start_bit, n_cubes, E, spec && !c->opt_eg_no_resolve))) return rc;
         E.status_host = c->h_status_dev;  // the consumer hands the verdict to the host (nullptr: a copy)
         E.seq = ++c->egd_seq;
@@ -1301,7 +1301,7 @@ int dct3d_decode_eg(dct3d_ctx* c, const uint8_t* bytes, uint64_t nbytes, int sta
     if ((rc = c->d_egd_in.grow((nbytes + 8) & ~(uint64_t)3))) return rc;
     if (hipMemcpyAsync(c->d_egd_in.p, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return DCT3D_EDEVICE;
     for (int spec = 1;; spec = 0) {
-        EgDecParams E;
+        EgDecParams E{};
         if ((rc = eg_decode_front(c, (const uint8_t*)c->d_egd_in.p, nbytes, (uint64_t)start_bit, n_cubes, E,
                                   spec && !c->opt_eg_no_resolve)))
             return rc;
